@@ -1,0 +1,476 @@
+// hsflow_api.cpp -- the C ABI declared in include/hsflow.h.
+//
+// Host side of the drop-in boundary for HornSchunckOF/hornSchunck.cpp:
+//   getFlow      (hornSchunck.cpp:43-75) -> hsflow_flow / hsflow_flow_device
+//   getGradients (hornSchunck.cpp:19-41) -> hsflow_gradients / *_device
+// Context = device + stream + grow-only device buffers, so repeated getFlow
+// calls on same-size frames (main.cpp:97-98 in a loop) never reallocate.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hsflow.h"
+#include "hsflow_internal.h"
+
+using hsflow::JacobiArgs;
+
+struct hsflow_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // device buffers (grow-only)
+    void *d_in = nullptr;
+    size_t d_in_bytes = 0;  // holds I0 and I1
+    void *d_out = nullptr;
+    size_t d_out_bytes = 0;  // holds u, v (or gx, gy, gt)
+    void *d_ws = nullptr;
+    size_t d_ws_bytes = 0;
+    // pinned host staging for the f32 results
+    float *h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;  // errors from calls without a context
+int g_kb_override = 0;
+
+int fail(hsflow_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx)
+        ctx->err = buf;
+    else
+        g_err = buf;
+    return code;
+}
+
+int hip_fail(hsflow_ctx *ctx, hipError_t e, const char *what) {
+    return fail(ctx, e == hipErrorOutOfMemory ? HSFLOW_ERR_OOM : HSFLOW_ERR_HIP,
+                "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+#define HIP_TRY(ctx, expr)                                    \
+    do {                                                      \
+        hipError_t e_ = (expr);                               \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+    } while (0)
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+// Largest frame: plane bytes must fit the 31-bit buffer offsets of K2.
+constexpr long long kMaxPlanePixels = (1ll << 29) - 1;
+
+bool sizes_ok(int rows, int cols, int batch) {
+    return rows >= 1 && cols >= 1 && batch >= 1 &&
+           (long long)rows * cols <= kMaxPlanePixels;
+}
+
+struct Workspace {
+    uint32_t *gpack;
+    float *gx, *gy, *gt, *u2, *v2;
+    uint32_t *flags;
+    size_t bytes;
+};
+
+Workspace carve(void *base, int rows, int cols, int batch) {
+    const size_t n = (size_t)rows * cols * batch;
+    Workspace w{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes);
+        return (char *)base + o;
+    };
+    w.gpack = (uint32_t *)take(n * 4);
+    w.gx = (float *)take(n * 4);
+    w.gy = (float *)take(n * 4);
+    w.gt = (float *)take(n * 4);
+    w.u2 = (float *)take(n * 4);
+    w.v2 = (float *)take(n * 4);
+    w.flags = (uint32_t *)take((size_t)batch * 4);
+    w.bytes = off;
+    return w;
+}
+
+int elem_size(int dtype) {
+    switch (dtype) {
+    case HSFLOW_U8: return 1;
+    case HSFLOW_F32: return 4;
+    case HSFLOW_F64: return 8;
+    default: return 0;
+    }
+}
+
+int pick_kb(int window, bool need_f32) {
+    if (window > 9) return 1;
+    if (g_kb_override > 0 && hsflow::kb_supported(window, g_kb_override, need_f32))
+        return g_kb_override;
+    int kb = hsflow::default_kb(window);
+    while (kb > 1 && !hsflow::kb_supported(window, kb, need_f32)) kb /= 2;
+    return kb;
+}
+
+int jacobi_impl(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int iters,
+                float alpha, bool warm, bool maybe_f32, float *u, float *v,
+                void *workspace, size_t ws_bytes, hipStream_t s) {
+    if (!sizes_ok(rows, cols, batch))
+        return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
+    if (window < 1 || window > HSFLOW_MAX_WINDOW)
+        return fail(ctx, HSFLOW_ERR_ARG, "windowSize %d outside [1, %d]", window,
+                    HSFLOW_MAX_WINDOW);
+    if (iters < 0) return fail(ctx, HSFLOW_ERR_ARG, "maxIterations %d < 0", iters);
+    if (!u || !v || !workspace) return fail(ctx, HSFLOW_ERR_ARG, "null device pointer");
+    Workspace w = carve(workspace, rows, cols, batch);
+    if (ws_bytes < w.bytes)
+        return fail(ctx, HSFLOW_ERR_ARG, "workspace %zu < %zu bytes", ws_bytes, w.bytes);
+    const size_t n = (size_t)rows * cols * batch;
+    if (iters == 0) {
+        // hornSchunck.cpp:49-50: the loop does not run, u = v = 0
+        if (!warm) {
+            HIP_TRY(ctx, hipMemsetAsync(u, 0, n * 4, s));
+            HIP_TRY(ctx, hipMemsetAsync(v, 0, n * 4, s));
+        }
+        return HSFLOW_OK;
+    }
+    const int kb = pick_kb(window, maybe_f32);
+    const int passes = (iters + kb - 1) / kb;
+    JacobiArgs a{};
+    a.rows = rows;
+    a.cols = cols;
+    a.batch = batch;
+    a.alpha2 = (float)((double)alpha * (double)alpha);  // pow(alpha, 2)
+    a.inv_w2 = (float)(1.0 / ((double)window * (double)window));
+    a.gpack = w.gpack;
+    a.gx = w.gx;
+    a.gy = w.gy;
+    a.gt = w.gt;
+    a.flags = w.flags;
+    // pass p writes the caller's buffers iff (passes-1-p) is even, so the
+    // last pass always lands in (u, v)
+    auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };
+    const float *src_u = nullptr, *src_v = nullptr;
+    if (warm) {
+        if (dst_is_user(0)) {  // would read and write (u, v) in one pass
+            HIP_TRY(ctx, hipMemcpyAsync(w.u2, u, n * 4, hipMemcpyDeviceToDevice, s));
+            HIP_TRY(ctx, hipMemcpyAsync(w.v2, v, n * 4, hipMemcpyDeviceToDevice, s));
+            src_u = w.u2;
+            src_v = w.v2;
+        } else {
+            src_u = u;
+            src_v = v;
+        }
+    }
+    int done = 0;
+    for (int pass = 0; pass < passes; ++pass) {
+        a.iters = std::min(kb, iters - done);
+        a.u_in = src_u;
+        a.v_in = src_v;
+        a.u_out = dst_is_user(pass) ? u : w.u2;
+        a.v_out = dst_is_user(pass) ? v : w.v2;
+        hipError_t e = hsflow::launch_jacobi(a, window, kb, s);
+        if (e != hipSuccess) return hip_fail(ctx, e, "jacobi launch");
+        src_u = a.u_out;
+        src_v = a.v_out;
+        done += a.iters;
+    }
+    return HSFLOW_OK;
+}
+
+int gradients_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
+                   int rows, int cols, int batch, float *gx, float *gy, float *gt,
+                   void *workspace, size_t ws_bytes, hipStream_t s) {
+    if (!sizes_ok(rows, cols, batch))
+        return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
+    if (dtype_in != HSFLOW_U8 && dtype_in != HSFLOW_F32)
+        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8 or F32");
+    if (!I0 || !I1 || !workspace) return fail(ctx, HSFLOW_ERR_ARG, "null device pointer");
+    Workspace w = carve(workspace, rows, cols, batch);
+    if (ws_bytes < w.bytes)
+        return fail(ctx, HSFLOW_ERR_ARG, "workspace %zu < %zu bytes", ws_bytes, w.bytes);
+    HIP_TRY(ctx, hipMemsetAsync(w.flags, 0, (size_t)batch * 4, s));
+    hipError_t e = hsflow::launch_gradients(I0, I1, dtype_in, rows, cols, batch, w.gpack,
+                                            w.gx, w.gy, w.gt, w.flags, s);
+    if (e != hipSuccess) return hip_fail(ctx, e, "gradients launch");
+    const size_t n = (size_t)rows * cols * batch;
+    if (gx) HIP_TRY(ctx, hipMemcpyAsync(gx, w.gx, n * 4, hipMemcpyDeviceToDevice, s));
+    if (gy) HIP_TRY(ctx, hipMemcpyAsync(gy, w.gy, n * 4, hipMemcpyDeviceToDevice, s));
+    if (gt) HIP_TRY(ctx, hipMemcpyAsync(gt, w.gt, n * 4, hipMemcpyDeviceToDevice, s));
+    return HSFLOW_OK;
+}
+
+int grow(hsflow_ctx *ctx, void **p, size_t *have, size_t need) {
+    if (*have >= need) return HSFLOW_OK;
+    if (*p) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(*p));
+        *p = nullptr;
+        *have = 0;
+    }
+    HIP_TRY(ctx, hipMalloc(p, need));
+    *have = need;
+    return HSFLOW_OK;
+}
+
+int grow_host(hsflow_ctx *ctx, size_t need) {
+    if (ctx->h_stage_bytes >= need) return HSFLOW_OK;
+    if (ctx->h_stage) {
+        HIP_TRY(ctx, hipHostFree(ctx->h_stage));
+        ctx->h_stage = nullptr;
+        ctx->h_stage_bytes = 0;
+    }
+    HIP_TRY(ctx, hipHostMalloc((void **)&ctx->h_stage, need, hipHostMallocDefault));
+    ctx->h_stage_bytes = need;
+    return HSFLOW_OK;
+}
+
+// Host rows (any supported dtype, any step) -> dense device U8 or F32.
+// F64 input (CV_64FC1) is narrowed to f32 on the host first.
+int upload(hsflow_ctx *ctx, const void *src, int dtype, int rows, int cols, size_t step,
+           void *dst, int *dev_dtype) {
+    if (dtype == HSFLOW_U8 || dtype == HSFLOW_F32) {
+        const size_t es = (size_t)elem_size(dtype);
+        HIP_TRY(ctx, hipMemcpy2DAsync(dst, cols * es, src, step, cols * es, rows,
+                                      hipMemcpyHostToDevice, ctx->stream));
+        *dev_dtype = dtype;
+        return HSFLOW_OK;
+    }
+    // F64: narrow through the pinned stage
+    int rc = grow_host(ctx, (size_t)rows * cols * 4);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // stage may be in use
+    for (int r = 0; r < rows; ++r) {
+        const double *s = (const double *)((const char *)src + (size_t)r * step);
+        float *d = ctx->h_stage + (size_t)r * cols;
+        for (int c = 0; c < cols; ++c) d[c] = (float)s[c];
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(dst, ctx->h_stage, (size_t)rows * cols * 4,
+                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *dev_dtype = HSFLOW_F32;
+    return HSFLOW_OK;
+}
+
+// dense device f32 plane -> host rows of dtype_out with step `step`
+int download(hsflow_ctx *ctx, const float *src, int rows, int cols, void *dst,
+             int dtype_out, size_t step) {
+    if (dtype_out == HSFLOW_F32) {
+        HIP_TRY(ctx, hipMemcpy2DAsync(dst, step, src, (size_t)cols * 4, (size_t)cols * 4,
+                                      rows, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return HSFLOW_OK;
+    }
+    int rc = grow_host(ctx, (size_t)rows * cols * 4);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_stage, src, (size_t)rows * cols * 4,
+                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int r = 0; r < rows; ++r) {
+        double *d = (double *)((char *)dst + (size_t)r * step);
+        const float *s = ctx->h_stage + (size_t)r * cols;
+        for (int c = 0; c < cols; ++c) d[c] = (double)s[c];
+    }
+    return HSFLOW_OK;
+}
+
+int check_host_args(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
+                    int rows, int cols, size_t in_step, int dtype_out, size_t out_step) {
+    if (!ctx) return HSFLOW_ERR_ARG;
+    if (!I0 || !I1) return fail(ctx, HSFLOW_ERR_ARG, "null image");
+    if (!sizes_ok(rows, cols, 1))
+        return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d", rows, cols);
+    const int es = elem_size(dtype_in);
+    if (!es) return fail(ctx, HSFLOW_ERR_ARG, "unsupported input dtype %d", dtype_in);
+    if (in_step < (size_t)cols * es)
+        return fail(ctx, HSFLOW_ERR_ARG, "input step %zu < row bytes", in_step);
+    if (dtype_out != HSFLOW_F32 && dtype_out != HSFLOW_F64)
+        return fail(ctx, HSFLOW_ERR_ARG, "output dtype must be F32 or F64");
+    if (out_step < (size_t)cols * elem_size(dtype_out))
+        return fail(ctx, HSFLOW_ERR_ARG, "output step %zu < row bytes", out_step);
+    return HSFLOW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hsflow_version(void) { return HSFLOW_VERSION; }
+
+const char *hsflow_status_string(int status) {
+    switch (status) {
+    case HSFLOW_OK: return "ok";
+    case HSFLOW_ERR_ARG: return "invalid argument";
+    case HSFLOW_ERR_HIP: return "HIP runtime error";
+    case HSFLOW_ERR_OOM: return "device out of memory";
+    case HSFLOW_ERR_NODEV: return "no usable HIP device";
+    case HSFLOW_ERR_SIZE: return "image sizes differ";
+    default: return "unknown status";
+    }
+}
+
+int hsflow_create(hsflow_ctx **out, int device) {
+    if (!out) return fail(nullptr, HSFLOW_ERR_ARG, "null ctx pointer");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(nullptr, HSFLOW_ERR_NODEV, "no HIP device");
+    if (device < 0 || device >= n)
+        return fail(nullptr, HSFLOW_ERR_NODEV, "device %d of %d", device, n);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return fail(nullptr, HSFLOW_ERR_NODEV, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, HSFLOW_ERR_NODEV, "device %d is %s, libhsflow is built for gfx950",
+                    device, prop.gcnArchName);
+    hsflow_ctx *ctx = new hsflow_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return fail(nullptr, HSFLOW_ERR_HIP, "stream creation failed");
+    }
+    *out = ctx;
+    return HSFLOW_OK;
+}
+
+void hsflow_destroy(hsflow_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_in) (void)hipFree(ctx->d_in);
+    if (ctx->d_out) (void)hipFree(ctx->d_out);
+    if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *hsflow_last_error(const hsflow_ctx *ctx) {
+    return ctx ? ctx->err.c_str() : g_err.c_str();
+}
+
+void *hsflow_stream(hsflow_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+size_t hsflow_workspace_bytes(int rows, int cols, int batch) {
+    if (!sizes_ok(rows, cols, batch)) return 0;
+    return carve(nullptr, rows, cols, batch).bytes;
+}
+
+int hsflow_set_iters_per_launch(int k) {
+    if (k < 0) return HSFLOW_ERR_ARG;
+    g_kb_override = k;
+    return HSFLOW_OK;
+}
+
+int hsflow_iters_per_launch(int rows, int cols, int batch, int window) {
+    (void)rows;
+    (void)cols;
+    (void)batch;
+    if (window < 1 || window > HSFLOW_MAX_WINDOW) return HSFLOW_ERR_ARG;
+    return pick_kb(window, true);
+}
+
+int hsflow_gradients_device(const void *I0, const void *I1, int dtype_in, int rows,
+                            int cols, int batch, float *gx, float *gy, float *gt,
+                            void *workspace, size_t workspace_bytes, void *stream) {
+    return gradients_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, gx, gy, gt,
+                          workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
+                         float alpha, int warm_start, float *u, float *v, void *workspace,
+                         size_t workspace_bytes, void *stream) {
+    // the workspace flags say per pair which gradient format is valid; the
+    // f32 variant is launched too unless we know every pair is packed
+    return jacobi_impl(nullptr, rows, cols, batch, window, iters, alpha, warm_start != 0,
+                       true, u, v, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int hsflow_flow_device(const void *I0, const void *I1, int dtype_in, int rows, int cols,
+                       int batch, int window, int iters, float alpha, float *u, float *v,
+                       void *workspace, size_t workspace_bytes, void *stream) {
+    int rc = gradients_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, nullptr,
+                            nullptr, nullptr, workspace, workspace_bytes,
+                            (hipStream_t)stream);
+    if (rc) return rc;
+    // 8-bit inputs always give exact packed gradients: skip the f32 variant
+    return jacobi_impl(nullptr, rows, cols, batch, window, iters, alpha, false,
+                       dtype_in != HSFLOW_U8, u, v, workspace, workspace_bytes,
+                       (hipStream_t)stream);
+}
+
+int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, int rows,
+                int cols, size_t in_step, int window, int iters, double alpha, void *u,
+                void *v, int dtype_out, size_t out_step) {
+    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step, dtype_out,
+                             out_step);
+    if (rc) return rc;
+    if (!u || !v) return fail(ctx, HSFLOW_ERR_ARG, "null output");
+    if (window < 1 || window > HSFLOW_MAX_WINDOW)
+        return fail(ctx, HSFLOW_ERR_ARG, "windowSize %d outside [1, %d]", window,
+                    HSFLOW_MAX_WINDOW);
+    if (iters < 0) return fail(ctx, HSFLOW_ERR_ARG, "maxIterations %d < 0", iters);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)rows * cols;
+    const size_t in_es = dtype_in == HSFLOW_U8 ? 1 : 4;
+    if ((rc = grow(ctx, &ctx->d_in, &ctx->d_in_bytes, align_up(n * in_es) * 2))) return rc;
+    if ((rc = grow(ctx, &ctx->d_out, &ctx->d_out_bytes, align_up(n * 4) * 3))) return rc;
+    const size_t wsb = hsflow_workspace_bytes(rows, cols, 1);
+    if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, wsb))) return rc;
+    char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
+    float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
+    int dt0 = 0, dt1 = 0;
+    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step, in0, &dt0))) return rc;
+    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step, in1, &dt1))) return rc;
+    rc = gradients_impl(ctx, in0, in1, dt0, rows, cols, 1, nullptr, nullptr, nullptr,
+                        ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
+    if (rc) return rc;
+    rc = jacobi_impl(ctx, rows, cols, 1, window, iters, (float)alpha, false,
+                     dt0 != HSFLOW_U8, du, dv, ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
+    if (rc) return rc;
+    if ((rc = download(ctx, du, rows, cols, u, dtype_out, out_step))) return rc;
+    if ((rc = download(ctx, dv, rows, cols, v, dtype_out, out_step))) return rc;
+    return HSFLOW_OK;
+}
+
+int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
+                     int rows, int cols, size_t in_step, void *gx, void *gy, void *gt,
+                     int dtype_out, size_t out_step) {
+    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step, dtype_out,
+                             out_step);
+    if (rc) return rc;
+    if (!gx || !gy || !gt) return fail(ctx, HSFLOW_ERR_ARG, "null output");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)rows * cols;
+    const size_t in_es = dtype_in == HSFLOW_U8 ? 1 : 4;
+    if ((rc = grow(ctx, &ctx->d_in, &ctx->d_in_bytes, align_up(n * in_es) * 2))) return rc;
+    if ((rc = grow(ctx, &ctx->d_out, &ctx->d_out_bytes, align_up(n * 4) * 3))) return rc;
+    const size_t wsb = hsflow_workspace_bytes(rows, cols, 1);
+    if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, wsb))) return rc;
+    char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
+    float *dx = (float *)ctx->d_out;
+    float *dy = (float *)((char *)dx + align_up(n * 4));
+    float *dt = (float *)((char *)dy + align_up(n * 4));
+    int dt0 = 0, dt1 = 0;
+    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step, in0, &dt0))) return rc;
+    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step, in1, &dt1))) return rc;
+    rc = gradients_impl(ctx, in0, in1, dt0, rows, cols, 1, dx, dy, dt, ctx->d_ws,
+                        ctx->d_ws_bytes, ctx->stream);
+    if (rc) return rc;
+    if ((rc = download(ctx, dx, rows, cols, gx, dtype_out, out_step))) return rc;
+    if ((rc = download(ctx, dy, rows, cols, gy, dtype_out, out_step))) return rc;
+    if ((rc = download(ctx, dt, rows, cols, gt, dtype_out, out_step))) return rc;
+    return HSFLOW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,29 @@
+// hsflow_internal.h -- shared between the kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hsflow {
+
+// Arguments of one Jacobi launch (hornSchunck.cpp:56-74 x `iters`).
+struct JacobiArgs {
+    int rows, cols, batch;
+    int iters;             // iterations fused in this launch (<= KB)
+    int tiles_x, tiles_y;  // filled by the launcher
+    float alpha2;          // pow(alpha, 2)            (hornSchunck.cpp:68)
+    float inv_w2;          // 1 / pow(windowSize, 2)   (hornSchunck.cpp:53)
+    const float *u_in, *v_in;  // nullptr -> initial state u = v = 0 (:49-50)
+    float *u_out, *v_out;
+    const uint32_t *gpack;     // packed exact integer gradients
+    const float *gx, *gy, *gt; // f32 gradients (non-integral inputs)
+    const uint32_t *flags;     // per pair: 0 -> gpack valid, else f32 planes
+};
+
+hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
+                            int cols, int batch, uint32_t *gpack, float *gx, float *gy,
+                            float *gt, uint32_t *flags, hipStream_t s);
+hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s);
+int default_kb(int W);
+bool kb_supported(int W, int KB, bool need_f32);
+
+}  // namespace hsflow

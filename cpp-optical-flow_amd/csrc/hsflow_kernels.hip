@@ -1,0 +1,427 @@
+// hsflow_kernels.hip -- CDNA4 (gfx950) kernels of the Horn-Schunck hot path.
+//
+// Replaces the numeric body of HornSchunckOF/hornSchunck.cpp:19-75 (the
+// reference runs it as ~15 OpenCV full-image float64 passes per iteration,
+// SURVEY.md §2.1).  Two kernels:
+//
+//  K1 hs_gradients_kernel   hornSchunck.cpp:19-41, once per pair.
+//     Sobel Ix, Iy on I0 (reflect-101) and It = I1 - I0.  For 8-bit-valued
+//     inputs these are small integers (|Ix|,|Iy| <= 1020, |It| <= 255) and are
+//     packed EXACTLY into one 32-bit word (11+11+9 bit two's complement), so
+//     the Jacobi loop streams 4 B of gradients per pixel instead of 12.
+//     Non-integral f32 inputs set a per-pair flag; K2 then takes an f32-plane
+//     branch for that pair (same launch, shorter regions).
+//
+//  K2 hs_jacobi_kernel      hornSchunck.cpp:56-74, the hot loop.
+//     Register-resident, temporally blocked stencil: one wavefront owns a
+//     64-column x RH-row region of (u, v, packed gradients) held in VGPRs
+//     (lane = column, unrolled row arrays), runs KB Jacobi iterations on it
+//     without touching memory (horizontal box sums by cross-lane permutes,
+//     vertical sums by a W-deep register ring, in-place row update), and
+//     writes back the interior (64 - KB(W-1)) x (RH - KB(W-1)) tile.  Halo =
+//     KB * anchor extents; outside the image u = v = 0 (BORDER_CONSTANT,
+//     hornSchunck.cpp:60-61) is re-imposed after every iteration.  No LDS, no
+//     barriers: every wave is independent.  Ping-pong u/v buffers between
+//     launches.  Results are bit-identical for every KB (same per-pixel
+//     operation sequence), which the tests check.
+//
+//  K2g hs_jacobi_generic_kernel   any window up to HSFLOW_MAX_WINDOW, one
+//     iteration per launch, direct sums from L1/L2.  Used for windows > 9.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hsflow_internal.h"
+
+namespace hsflow {
+
+// ------------------------------------------------------------------ packing
+__device__ __forceinline__ uint32_t pack_grad(int ix, int iy, int it) {
+    return ((uint32_t)ix & 0x7FFu) | (((uint32_t)iy & 0x7FFu) << 11) |
+           (((uint32_t)it & 0x1FFu) << 22);
+}
+__device__ __forceinline__ void unpack_grad(uint32_t p, float &ix, float &iy,
+                                            float &it) {
+    ix = (float)__builtin_amdgcn_sbfe(p, 0, 11);
+    iy = (float)__builtin_amdgcn_sbfe(p, 11, 11);
+    it = (float)__builtin_amdgcn_sbfe(p, 22, 9);
+}
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    // OpenCV borderInterpolate(BORDER_REFLECT_101) for |overshoot| <= 1.
+    if (len == 1) return 0;
+    p = p < 0 ? -p : p;
+    return p >= len ? 2 * (len - 1) - p : p;
+}
+
+template <typename T> __device__ __forceinline__ float ld_px(const T *p) {
+    return (float)*p;
+}
+
+// ----------------------------------------------------------------------- K1
+// block 64 x 4, one pixel per thread; grid (ceil(cols/64), ceil(rows/4), batch)
+template <typename T>
+__global__ __launch_bounds__(256) void hs_gradients_kernel(
+    const T *__restrict__ I0, const T *__restrict__ I1, int rows, int cols,
+    uint32_t *__restrict__ gpack, float *__restrict__ gx, float *__restrict__ gy,
+    float *__restrict__ gt, uint32_t *__restrict__ flags) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const int r = blockIdx.y * 4 + threadIdx.y;
+    const size_t plane = (size_t)rows * cols;
+    const T *a = I0 + blockIdx.z * plane;
+    const T *b = I1 + blockIdx.z * plane;
+    bool bad = false;
+    if (r < rows && c < cols) {
+        const int rm = reflect101(r - 1, rows), rp = reflect101(r + 1, rows);
+        const int cm = reflect101(c - 1, cols), cp = reflect101(c + 1, cols);
+        const T *pm = a + (size_t)rm * cols, *p0 = a + (size_t)r * cols,
+                *pp = a + (size_t)rp * cols;
+        const float m_m = ld_px(pm + cm), m_0 = ld_px(pm + c), m_p = ld_px(pm + cp);
+        const float z_m = ld_px(p0 + cm), z_0 = ld_px(p0 + c), z_p = ld_px(p0 + cp);
+        const float p_m = ld_px(pp + cm), p_0 = ld_px(pp + c), p_p = ld_px(pp + cp);
+        const float nxt = ld_px(b + (size_t)r * cols + c);
+        // hornSchunck.cpp:27-28 (Sobel ksize 3) and :39; exact for 8-bit data
+        const float dx = (m_p - m_m) + 2.0f * (z_p - z_m) + (p_p - p_m);
+        const float dy = (p_m - m_m) + 2.0f * (p_0 - m_0) + (p_p - m_p);
+        const float dt = nxt - z_0;
+        const size_t o = blockIdx.z * plane + (size_t)r * cols + c;
+        gx[o] = dx;
+        gy[o] = dy;
+        gt[o] = dt;
+        // packed form is exact iff both frames are integers in [0, 255]
+        bad = !(z_0 == rintf(z_0) && nxt == rintf(nxt) && z_0 >= 0.f && z_0 <= 255.f &&
+                nxt >= 0.f && nxt <= 255.f);
+        gpack[o] = pack_grad((int)dx, (int)dy, (int)dt);
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[blockIdx.z], 1u);
+}
+
+// ----------------------------------------------------------------------- K2
+// value of x held by lane (lane + D) of this wavefront (wraps at 64; callers
+// only use wrapped results in the invalid halo)
+template <int D> __device__ __forceinline__ float lane_rel(float x, int lane) {
+    if constexpr (D == 0) {
+        return x;
+    } else {
+        return __int_as_float(
+            __builtin_amdgcn_ds_bpermute(((lane + D) & 63) << 2, __float_as_int(x)));
+    }
+}
+
+template <int W, int D = -(W - W / 2 - 1)>
+__device__ __forceinline__ float hsum(float x, int lane) {
+    // sum over lanes lane-A .. lane+W-1-A, left to right (A = anchor)
+    constexpr int A = W - W / 2 - 1;
+    if constexpr (D == W - 1 - A) {
+        return lane_rel<D>(x, lane);
+    } else {
+        return lane_rel<D>(x, lane) + hsum<W, D + 1>(x, lane);
+    }
+}
+
+// Keep the compiler from CSE-ing an address computation across the
+// iteration loop (that would pin RH extra VGPRs for the whole solve).
+__device__ __forceinline__ int launder(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ uint32_t launder_u(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ float launder_f(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// One wavefront's work on one region: rows [r0, r0 + RH) x the 64 columns
+// starting at gc - lane; KB iterations; writes region rows [HL, HL + nout)
+// (nout <= RH - HL - HR) of the lanes [HL, 64 - HR).
+template <int W, int KB, int RH, bool PACKED>
+__device__ __forceinline__ void jacobi_region(const JacobiArgs &p, size_t pbase,
+                                              int plane_bytes, int lane, int gc, int r0,
+                                              int nout) {
+    constexpr int A = W - W / 2 - 1;  // anchor (hornSchunck.cpp:54)
+    constexpr int AR = W - 1 - A;     // taps right/below of the anchor
+    constexpr int HL = KB * A, HR = KB * AR;
+    constexpr int OX = 64 - HL - HR;
+    static_assert(OX > 0 && RH - HL - HR > 0, "halo too deep for the region");
+    static_assert(RH <= 64, "row mask is 64 bits");
+    const int cols = p.cols;
+    const bool col_in = (unsigned)gc < (unsigned)cols;
+    // bit r set <=> region row r lies inside the image (wave-uniform)
+    uint64_t rowmask = 0;
+#pragma unroll
+    for (int r = 0; r < RH; ++r)
+        rowmask |= (uint64_t)((unsigned)(r0 + r) < (unsigned)p.rows) << r;
+
+    // Buffer descriptors over this pair's planes: a byte offset >= the
+    // plane size reads 0 / drops the store, so the halo outside the image
+    // (u = v = 0, BORDER_CONSTANT) needs no branches.
+    constexpr int kOOB = 0x7FFFFFF0;
+    const auto u_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase), 0, p.u_in ? plane_bytes : 0,
+        0x00020000);
+    const auto v_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(p.v_in ? p.v_in + pbase : p.v_out + pbase), 0, p.v_in ? plane_bytes : 0,
+        0x00020000);
+
+    float u[RH], v[RH];
+    uint32_t g[PACKED ? RH : 1];
+    float gxr[PACKED ? 1 : RH], gyr[PACKED ? 1 : RH], gtr[PACKED ? 1 : RH];
+    {
+        const auto g_rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.gpack + pbase), 0, PACKED ? plane_bytes : 0, 0x00020000);
+        const auto gx_rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.gx + pbase), 0, PACKED ? 0 : plane_bytes, 0x00020000);
+        const auto gy_rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.gy + pbase), 0, PACKED ? 0 : plane_bytes, 0x00020000);
+        const auto gt_rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.gt + pbase), 0, PACKED ? 0 : plane_bytes, 0x00020000);
+        const int off0 = (r0 * cols + gc) * 4;
+#pragma unroll
+        for (int r = 0; r < RH; ++r) {
+            const bool in = col_in && ((rowmask >> r) & 1ull);
+            const int off = in ? off0 + r * cols * 4 : kOOB;
+            u[r] = __builtin_amdgcn_raw_buffer_load_b32(u_rs, off, 0, 0);
+            v[r] = __builtin_amdgcn_raw_buffer_load_b32(v_rs, off, 0, 0);
+            if constexpr (PACKED) {
+                g[r] = __builtin_amdgcn_raw_buffer_load_b32(g_rs, off, 0, 0);
+            } else {
+                gxr[r] = __builtin_amdgcn_raw_buffer_load_b32(gx_rs, off, 0, 0);
+                gyr[r] = __builtin_amdgcn_raw_buffer_load_b32(gy_rs, off, 0, 0);
+                gtr[r] = __builtin_amdgcn_raw_buffer_load_b32(gt_rs, off, 0, 0);
+            }
+        }
+    }
+
+    const float alpha2 = p.alpha2, inv = p.inv_w2;
+    for (int it = 0; it < p.iters; ++it) {
+        float ru[W], rv[W];  // ring of horizontal sums, compile-time indexed
+#pragma unroll
+        for (int r = 0; r < RH; ++r) {
+            ru[r % W] = hsum<W>(u[r], lane);
+            rv[r % W] = hsum<W>(v[r], lane);
+            const int y = r - AR;  // output row whose window ends at row r
+            if (y >= A) {
+                float su = 0.f, sv = 0.f;
+#pragma unroll
+                for (int d = 0; d < W; ++d) {
+                    su += ru[(y - A + d) % W];
+                    sv += rv[(y - A + d) % W];
+                }
+                const float ub = su * inv, vb = sv * inv;
+                float ix, iy, itv;
+                if constexpr (PACKED) {
+                    // unpack every iteration: hoisting the loop-invariant
+                    // Ix, Iy, It, 1/D out of the loop costs 4 VGPRs per row
+                    unpack_grad(launder_u(g[y]), ix, iy, itv);
+                } else {
+                    ix = launder_f(gxr[y]);
+                    iy = launder_f(gyr[y]);
+                    itv = launder_f(gtr[y]);
+                }
+                // hornSchunck.cpp:63-73
+                const float den = alpha2 + ix * ix + iy * iy;
+                const float num = ix * ub + iy * vb + itv;
+                const float cc = num * __builtin_amdgcn_rcpf(den);
+                const bool in = col_in && ((rowmask >> y) & 1ull);
+                u[y] = in ? ub - ix * cc : 0.f;
+                v[y] = in ? vb - iy * cc : 0.f;
+            }
+            // Keep rows in program order: otherwise the scheduler hoists every
+            // row's horizontal sums (they only read the previous iteration)
+            // and the live set explodes past 256 VGPRs.
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    {
+        const auto uo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_out + pbase), 0,
+                                                             plane_bytes, 0x00020000);
+        const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
+                                                             plane_bytes, 0x00020000);
+        const bool st_lane = lane >= HL && lane < HL + OX && col_in;
+        const int off0 = launder(((r0 + HL) * cols + gc) * 4);
+#pragma unroll
+        for (int r = HL; r < RH - HR; ++r) {
+            const bool in = st_lane && (r - HL) < nout && ((rowmask >> r) & 1ull);
+            const int off = in ? off0 + (r - HL) * cols * 4 : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b32(u[r], uo_rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(v[r], vo_rs, off, 0, 0);
+        }
+    }
+}
+
+// Region heights (rows held in VGPRs per wavefront).
+constexpr int kRowsPacked = 48;
+constexpr int kRowsF32 = 24;
+constexpr bool kb_ok_packed(int W, int KB) { return KB * (W - 1) <= 32; }
+constexpr bool kb_ok_f32(int W, int KB) { return KB * (W - 1) <= 16; }
+
+// f32-gradient path (pairs whose inputs are not 8-bit integers): 5 VGPRs per
+// region row, so it walks the packed tile in 24-row regions and the kernel's
+// register budget (the max over both branches) stays that of the packed path.
+template <int W, int KB>
+__device__ __forceinline__ void jacobi_tile_f32(const JacobiArgs p, size_t pbase,
+                                                         int plane_bytes, int lane, int gc,
+                                                         int out_r0, int nout) {
+    if constexpr (kb_ok_f32(W, KB)) {
+        constexpr int HL = KB * (W - W / 2 - 1);
+        constexpr int OYF = kRowsF32 - KB * (W - 1);
+        for (int o = 0; o < nout; o += OYF)
+            jacobi_region<W, KB, kRowsF32, false>(p, pbase, plane_bytes, lane, gc,
+                                                  out_r0 + o - HL, min(OYF, nout - o));
+    }
+}
+
+template <int W, int KB>
+__global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
+    constexpr int HL = KB * (W - W / 2 - 1);
+    constexpr int OX = 64 - KB * (W - 1), OY = kRowsPacked - KB * (W - 1);
+    const int pair = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform tile index (readfirstlane: keep tile maths in SGPRs)
+    const int tile =
+        blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (tile >= p.tiles_x * p.tiles_y) return;
+    const int ty = tile / p.tiles_x, tx = tile - ty * p.tiles_x;
+    const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)p.cols;
+    const int plane_bytes = p.rows * p.cols * 4;
+    const int gc = tx * OX - HL + lane;  // this lane's image column
+    const uint32_t flag = p.flags != nullptr ? p.flags[pair] : 0u;
+    if (flag != 0u) {
+        jacobi_tile_f32<W, KB>(p, pbase, plane_bytes, lane, gc, ty * OY, OY);
+        return;
+    }
+    jacobi_region<W, KB, kRowsPacked, true>(p, pbase, plane_bytes, lane, gc, ty * OY - HL,
+                                            OY);
+}
+
+// ---------------------------------------------------------------------- K2g
+__global__ __launch_bounds__(256) void hs_jacobi_generic_kernel(const JacobiArgs p,
+                                                                int W) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int pair = blockIdx.z;
+    if (r >= p.rows || c >= p.cols) return;
+    const int A = W - W / 2 - 1;
+    const size_t plane = (size_t)p.rows * p.cols;
+    const size_t pbase = (size_t)pair * plane;
+    float su = 0.f, sv = 0.f;
+    if (p.u_in) {
+        for (int i = 0; i < W; ++i) {
+            const int yy = r + i - A;
+            if ((unsigned)yy >= (unsigned)p.rows) continue;
+            float hu = 0.f, hv = 0.f;
+            for (int j = 0; j < W; ++j) {
+                const int xx = c + j - A;
+                if ((unsigned)xx >= (unsigned)p.cols) continue;
+                hu += p.u_in[pbase + (size_t)yy * p.cols + xx];
+                hv += p.v_in[pbase + (size_t)yy * p.cols + xx];
+            }
+            su += hu;
+            sv += hv;
+        }
+    }
+    const size_t o = pbase + (size_t)r * p.cols + c;
+    float ix, iy, itv;
+    if (p.flags != nullptr && p.flags[pair] != 0u) {
+        ix = p.gx[o];
+        iy = p.gy[o];
+        itv = p.gt[o];
+    } else {
+        unpack_grad(p.gpack[o], ix, iy, itv);
+    }
+    const float ub = su * p.inv_w2, vb = sv * p.inv_w2;
+    const float den = p.alpha2 + ix * ix + iy * iy;
+    const float num = ix * ub + iy * vb + itv;
+    const float cc = num * __builtin_amdgcn_rcpf(den);
+    p.u_out[o] = ub - ix * cc;
+    p.v_out[o] = vb - iy * cc;
+}
+
+// ------------------------------------------------------------------ launchers
+hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
+                            int cols, int batch, uint32_t *gpack, float *gx, float *gy,
+                            float *gt, uint32_t *flags, hipStream_t s) {
+    dim3 blk(64, 4, 1), grd((cols + 63) / 64, (rows + 3) / 4, batch);
+    if (dtype_in == 0)
+        hipLaunchKernelGGL(hs_gradients_kernel<uint8_t>, grd, blk, 0, s,
+                           (const uint8_t *)I0, (const uint8_t *)I1, rows, cols, gpack,
+                           gx, gy, gt, flags);
+    else
+        hipLaunchKernelGGL(hs_gradients_kernel<float>, grd, blk, 0, s,
+                           (const float *)I0, (const float *)I1, rows, cols, gpack, gx,
+                           gy, gt, flags);
+    return hipGetLastError();
+}
+
+template <int W, int KB>
+static hipError_t launch_jacobi_t(JacobiArgs a, hipStream_t s) {
+    constexpr int OX = 64 - KB * (W - 1), OY = kRowsPacked - KB * (W - 1);
+    a.tiles_x = (a.cols + OX - 1) / OX;
+    a.tiles_y = (a.rows + OY - 1) / OY;
+    const long ntiles = (long)a.tiles_x * a.tiles_y;
+    dim3 grd((unsigned)((ntiles + 3) / 4), (unsigned)a.batch, 1);
+    hipLaunchKernelGGL((hs_jacobi_kernel<W, KB>), grd, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// Temporal-blocking depth per window: largest KB in {1,2,4,8} whose halo fits
+// 16 columns.  Overridable through hsflow_set_iters_per_launch().
+int default_kb(int W) {
+    if (W < 1 || W > 9) return 1;
+    for (int kb : {8, 4, 2})
+        if (kb_ok_f32(W, kb)) return kb;
+    return 1;
+}
+
+bool kb_supported(int W, int KB, bool need_f32) {
+    if (W < 1 || W > 9) return KB == 1;
+    if (KB != 1 && KB != 2 && KB != 4 && KB != 8) return false;
+    return need_f32 ? kb_ok_f32(W, KB) : kb_ok_packed(W, KB);
+}
+
+template <int W>
+static hipError_t launch_jacobi_w(JacobiArgs a, int KB, hipStream_t s) {
+    switch (KB) {
+    case 1: return launch_jacobi_t<W, 1>(a, s);
+    case 2:
+        if constexpr (kb_ok_packed(W, 2)) return launch_jacobi_t<W, 2>(a, s);
+        break;
+    case 4:
+        if constexpr (kb_ok_packed(W, 4)) return launch_jacobi_t<W, 4>(a, s);
+        break;
+    case 8:
+        if constexpr (kb_ok_packed(W, 8)) return launch_jacobi_t<W, 8>(a, s);
+        break;
+    default: break;
+    }
+    return hipErrorInvalidValue;
+}
+
+// One Jacobi pass of a.iters (<= KB) iterations.  Pairs flagged by K1 as
+// non-integral take the f32-gradient path inside the same launch; the caller
+// must then pick KB with kb_supported(W, KB, true).
+hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s) {
+    switch (W) {
+    case 1: return launch_jacobi_w<1>(a, KB, s);
+    case 2: return launch_jacobi_w<2>(a, KB, s);
+    case 3: return launch_jacobi_w<3>(a, KB, s);
+    case 4: return launch_jacobi_w<4>(a, KB, s);
+    case 5: return launch_jacobi_w<5>(a, KB, s);
+    case 6: return launch_jacobi_w<6>(a, KB, s);
+    case 7: return launch_jacobi_w<7>(a, KB, s);
+    case 8: return launch_jacobi_w<8>(a, KB, s);
+    case 9: return launch_jacobi_w<9>(a, KB, s);
+    default: {
+        if (a.iters != 1) return hipErrorInvalidValue;
+        dim3 grd((a.cols + 63) / 64, (a.rows + 3) / 4, a.batch);
+        hipLaunchKernelGGL(hs_jacobi_generic_kernel, grd, dim3(256), 0, s, a, W);
+        return hipGetLastError();
+    }
+    }
+}
+
+}  // namespace hsflow

@@ -1,0 +1,355 @@
+"""Python host binding of libhsflow.so (MI355X Horn-Schunck).
+
+Mirrors the reference's operator interface, HornSchunckOF/hornSchunck.cpp:
+
+    hs = hornSchunck(windowSize, maxIterations, alpha)      # :13-17
+    gx, gy, gt = hs.getGradients(imagePrev, imageNext)       # :19-41
+    u, v = hs.getFlow(imagePrev, imageNext)                  # :43-75
+
+with numpy arrays standing in for cv::Mat: inputs are 2-D uint8 / float32 /
+float64 (any row stride), outputs are float64 (CV_64FC1, what the reference
+returns and plotFlow.cpp:72-75 reads).  Also exposes the stream-ordered
+device entry points for torch tensors and the host utilities.
+
+Everything here calls the HIP path in libhsflow.so; there is no CPU fallback.
+If the library is missing or no gfx950 device is present, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+try:  # load torch's HIP runtime first so libhsflow binds to the same one
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the host API
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhsflow.so")
+
+HSFLOW_OK = 0
+HSFLOW_ERR_ARG = -1
+HSFLOW_ERR_HIP = -2
+HSFLOW_ERR_OOM = -3
+HSFLOW_ERR_NODEV = -4
+HSFLOW_ERR_SIZE = -5
+U8, F32, F64 = 0, 1, 2
+
+# every symbol include/hsflow.h declares
+EXPORTS = (
+    "hsflow_version", "hsflow_status_string", "hsflow_create", "hsflow_destroy",
+    "hsflow_last_error", "hsflow_stream", "hsflow_flow", "hsflow_gradients",
+    "hsflow_workspace_bytes", "hsflow_flow_device", "hsflow_gradients_device",
+    "hsflow_jacobi_device", "hsflow_set_iters_per_launch", "hsflow_iters_per_launch",
+    "hsflow_bgr_to_gray", "hsflow_synth_pair",
+)
+
+
+class HsflowError(RuntimeError):
+    """A non-zero hsflow status (the reference would throw cv::Exception)."""
+
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"hsflow status {status}: {msg}")
+        self.status = status
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "-j4"])
+    return LIB_PATH
+
+
+def lib():
+    """Load libhsflow.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `make -C {_HERE}` "
+                          "(or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    i = ctypes.c_int
+    L.hsflow_version.restype = i
+    L.hsflow_status_string.restype = ctypes.c_char_p
+    L.hsflow_status_string.argtypes = [i]
+    L.hsflow_create.argtypes = [ctypes.POINTER(_vp), i]
+    L.hsflow_destroy.argtypes = [_vp]
+    L.hsflow_destroy.restype = None
+    L.hsflow_last_error.argtypes = [_vp]
+    L.hsflow_last_error.restype = ctypes.c_char_p
+    L.hsflow_stream.argtypes = [_vp]
+    L.hsflow_stream.restype = _vp
+    L.hsflow_flow.argtypes = [_vp, _vp, _vp, i, i, i, _sz, i, i, ctypes.c_double,
+                              _vp, _vp, i, _sz]
+    L.hsflow_gradients.argtypes = [_vp, _vp, _vp, i, i, i, _sz, _vp, _vp, _vp, i, _sz]
+    L.hsflow_workspace_bytes.argtypes = [i, i, i]
+    L.hsflow_workspace_bytes.restype = _sz
+    L.hsflow_flow_device.argtypes = [_vp, _vp, i, i, i, i, i, i, ctypes.c_float,
+                                     _vp, _vp, _vp, _sz, _vp]
+    L.hsflow_gradients_device.argtypes = [_vp, _vp, i, i, i, i, _vp, _vp, _vp,
+                                          _vp, _sz, _vp]
+    L.hsflow_jacobi_device.argtypes = [i, i, i, i, i, ctypes.c_float, i, _vp, _vp,
+                                       _vp, _sz, _vp]
+    L.hsflow_set_iters_per_launch.argtypes = [i]
+    L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
+    L.hsflow_bgr_to_gray.argtypes = [_vp, i, i, _sz, _vp, _sz]
+    L.hsflow_synth_pair.argtypes = [ctypes.c_uint64, i, i, i, i, _vp, _vp, _vp, _vp]
+    _lib = L
+    return L
+
+
+def _check(rc: int, ctx=None):
+    if rc != HSFLOW_OK:
+        L = lib()
+        msg = L.hsflow_last_error(ctx).decode(errors="replace")
+        raise HsflowError(rc, msg or L.hsflow_status_string(rc).decode())
+
+
+def _dtype_code(a: np.ndarray) -> int:
+    if a.dtype == np.uint8:
+        return U8
+    if a.dtype == np.float32:
+        return F32
+    if a.dtype == np.float64:
+        return F64
+    raise HsflowError(HSFLOW_ERR_ARG, f"unsupported image dtype {a.dtype}")
+
+
+def _as_image(a) -> np.ndarray:
+    a = np.asarray(a)
+    if a.ndim != 2:
+        raise HsflowError(HSFLOW_ERR_ARG, "images must be single-channel 2-D "
+                          "(convert BGR with bgr_to_gray, as main.cpp:13-14 does)")
+    if a.strides[1] != a.itemsize or a.strides[0] < a.shape[1] * a.itemsize:
+        a = np.ascontiguousarray(a)
+    return a
+
+
+class Context:
+    """Device + stream + cached device buffers (hsflow_ctx)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        p = _vp()
+        rc = L.hsflow_create(ctypes.byref(p), int(device))
+        if rc != HSFLOW_OK:
+            raise HsflowError(rc, L.hsflow_last_error(None).decode(errors="replace"))
+        self._p = p
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._p
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().hsflow_destroy(self._p)
+            self._p = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def flow(self, I0, I1, window: int, iters: int, alpha: float, out_dtype=np.float64):
+        a, b = _as_image(I0), _as_image(I1)
+        if a.shape != b.shape:
+            raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
+        if a.dtype != b.dtype:
+            b = b.astype(a.dtype)
+        rows, cols = a.shape
+        u = np.empty((rows, cols), out_dtype)
+        v = np.empty((rows, cols), out_dtype)
+        code = F64 if u.dtype == np.float64 else F32
+        rc = lib().hsflow_flow(self._p, a.ctypes.data, b.ctypes.data, _dtype_code(a),
+                               rows, cols, a.strides[0], int(window), int(iters),
+                               float(alpha), u.ctypes.data, v.ctypes.data, code,
+                               u.strides[0])
+        _check(rc, self._p)
+        return u, v
+
+    def gradients(self, I0, I1, out_dtype=np.float64):
+        a, b = _as_image(I0), _as_image(I1)
+        if a.shape != b.shape:
+            raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
+        if a.dtype != b.dtype:
+            b = b.astype(a.dtype)
+        rows, cols = a.shape
+        gx, gy, gt = (np.empty((rows, cols), out_dtype) for _ in range(3))
+        code = F64 if gx.dtype == np.float64 else F32
+        rc = lib().hsflow_gradients(self._p, a.ctypes.data, b.ctypes.data, _dtype_code(a),
+                                    rows, cols, a.strides[0], gx.ctypes.data,
+                                    gy.ctypes.data, gt.ctypes.data, code, gx.strides[0])
+        _check(rc, self._p)
+        return gx, gy, gt
+
+
+_default_ctx = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+class hornSchunck:  # noqa: N801  (reference class name, hornSchunck.cpp:8)
+    """Drop-in mirror of `class hornSchunck` (hornSchunck.cpp:8-76)."""
+
+    def __init__(self, inpWindowSize: int, inpMaxIterations: int, inpAlpha: float,
+                 context: Context | None = None):
+        # hornSchunck.cpp:13-17 -- public fields, same names
+        self.windowSize = int(inpWindowSize)
+        self.maxIterations = int(inpMaxIterations)
+        self.alpha = float(inpAlpha)
+        self._ctx = context
+
+    def _c(self):
+        return self._ctx if self._ctx is not None else default_context()
+
+    def getGradients(self, imagePrev, imageNext, gradX=None, gradY=None, gradT=None):
+        """hornSchunck.cpp:19-41 -> (gradX, gradY, gradT) float64."""
+        gx, gy, gt = self._c().gradients(imagePrev, imageNext)
+        for dst, src in ((gradX, gx), (gradY, gy), (gradT, gt)):
+            if dst is not None:
+                dst[...] = src
+        return gx, gy, gt
+
+    def getFlow(self, imagePrev, imageNext, u=None, v=None):
+        """hornSchunck.cpp:43-75 -> (u, v) float64 (CV_64FC1)."""
+        uu, vv = self._c().flow(imagePrev, imageNext, self.windowSize,
+                                self.maxIterations, self.alpha)
+        if u is not None:
+            u[...] = uu
+        if v is not None:
+            v[...] = vv
+        return uu, vv
+
+
+def compute(I0, I1, alpha: float, nIter: int, windowSize: int = 5):
+    """compute(I0, I1, alpha, nIter) -> (u, v): the north-star convenience
+    wrapper over hornSchunck(windowSize, nIter, alpha).getFlow."""
+    return hornSchunck(windowSize, nIter, alpha).getFlow(I0, I1)
+
+
+# ------------------------------------------------------------ device (torch)
+def _stream_ptr(stream):
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream if torch is not None else None
+    return getattr(stream, "cuda_stream", stream)
+
+
+def workspace_bytes(rows: int, cols: int, batch: int = 1) -> int:
+    return int(lib().hsflow_workspace_bytes(rows, cols, batch))
+
+
+def alloc_workspace(rows: int, cols: int, batch: int = 1, device="cuda"):
+    n = workspace_bytes(rows, cols, batch)
+    return torch.empty(n, dtype=torch.uint8, device=device)
+
+
+def _tensor_dtype(t) -> int:
+    if t.dtype == torch.uint8:
+        return U8
+    if t.dtype == torch.float32:
+        return F32
+    raise HsflowError(HSFLOW_ERR_ARG, f"device input dtype {t.dtype} (want uint8/float32)")
+
+
+def _check_dense(t, shape, name):
+    if not t.is_cuda or not t.is_contiguous() or tuple(t.shape[-2:]) != tuple(shape):
+        raise HsflowError(HSFLOW_ERR_ARG, f"{name}: need a contiguous CUDA tensor "
+                          f"[..., {shape[0]}, {shape[1]}]")
+
+
+def flow_device(I0, I1, window: int, iters: int, alpha: float, u=None, v=None,
+                workspace=None, stream=None):
+    """Stream-ordered solve on torch CUDA tensors [B, H, W] (or [H, W]).
+    Returns (u, v) float32 tensors.  No host synchronisation."""
+    rows, cols = I0.shape[-2:]
+    batch = int(np.prod(I0.shape[:-2])) if I0.dim() > 2 else 1
+    _check_dense(I0, (rows, cols), "I0")
+    _check_dense(I1, (rows, cols), "I1")
+    if I1.dtype != I0.dtype or I1.shape != I0.shape:
+        raise HsflowError(HSFLOW_ERR_SIZE, "I0/I1 differ in shape or dtype")
+    if u is None:
+        u = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
+    if v is None:
+        v = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
+    if workspace is None:
+        workspace = alloc_workspace(rows, cols, batch, I0.device)
+    rc = lib().hsflow_flow_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0), rows,
+                                  cols, batch, int(window), int(iters), float(alpha),
+                                  u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
+                                  workspace.numel(), _stream_ptr(stream))
+    _check(rc)
+    return u, v
+
+
+def gradients_device(I0, I1, workspace, gx=None, gy=None, gt=None, stream=None):
+    rows, cols = I0.shape[-2:]
+    batch = int(np.prod(I0.shape[:-2])) if I0.dim() > 2 else 1
+    _check_dense(I0, (rows, cols), "I0")
+    _check_dense(I1, (rows, cols), "I1")
+    ptr = (lambda t: t.data_ptr() if t is not None else None)
+    rc = lib().hsflow_gradients_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
+                                       rows, cols, batch, ptr(gx), ptr(gy), ptr(gt),
+                                       workspace.data_ptr(), workspace.numel(),
+                                       _stream_ptr(stream))
+    _check(rc)
+
+
+def jacobi_device(rows, cols, batch, window, iters, alpha, u, v, workspace,
+                  warm_start=False, stream=None):
+    rc = lib().hsflow_jacobi_device(int(rows), int(cols), int(batch), int(window),
+                                    int(iters), float(alpha), int(bool(warm_start)),
+                                    u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
+                                    workspace.numel(), _stream_ptr(stream))
+    _check(rc)
+
+
+def set_iters_per_launch(k: int):
+    _check(lib().hsflow_set_iters_per_launch(int(k)))
+
+
+def iters_per_launch(rows, cols, batch, window) -> int:
+    return int(lib().hsflow_iters_per_launch(rows, cols, batch, window))
+
+
+# ------------------------------------------------------------------ host utils
+def bgr_to_gray(bgr) -> np.ndarray:
+    """main.cpp:13-14 cvtColor(BGR2GRAY), OpenCV 4.x 15-bit fixed point."""
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    if bgr.ndim != 3 or bgr.shape[2] != 3:
+        raise HsflowError(HSFLOW_ERR_ARG, "need H x W x 3 BGR uint8")
+    rows, cols = bgr.shape[:2]
+    out = np.empty((rows, cols), np.uint8)
+    _check(lib().hsflow_bgr_to_gray(bgr.ctypes.data, rows, cols, bgr.strides[0],
+                                    out.ctypes.data, out.strides[0]))
+    return out
+
+
+def synth_pair(seed: int, rows: int, cols: int, qdy: int = -3, qdx: int = 6,
+               dtype=np.float32):
+    """Deterministic synthetic pair: motion (dy, dx) = (qdy, qdx)/4
+    px, default (-0.75, +1.5).  Seed convention: 1000 + pair index."""
+    I0 = np.empty((rows, cols), dtype)
+    I1 = np.empty((rows, cols), dtype)
+    if dtype == np.float32:
+        args = (I0.ctypes.data, I1.ctypes.data, None, None)
+    elif dtype == np.uint8:
+        args = (None, None, I0.ctypes.data, I1.ctypes.data)
+    else:
+        raise HsflowError(HSFLOW_ERR_ARG, "synth dtype must be float32 or uint8")
+    _check(lib().hsflow_synth_pair(int(seed), rows, cols, int(qdy), int(qdx), *args))
+    return I0, I1

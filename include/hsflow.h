@@ -1,0 +1,138 @@
+/*
+ * hsflow.h -- C ABI of libhsflow.so, the MI355X-native Horn-Schunck solver.
+ *
+ * Drop-in boundary.  The reference (liuyang9609/Cpp-Optical-Flow) exposes
+ * its hot path as a header-style C++ class compiled into the caller
+ * (HornSchunckOF/hornSchunck.cpp:8-76, pulled in by main.cpp:8):
+ *
+ *   hornSchunck(int windowSize, int maxIterations, double alpha)   :13-17
+ *   void getGradients(cv::Mat prev, cv::Mat next,
+ *                     cv::Mat& gx, cv::Mat& gy, cv::Mat& gt)       :19-41
+ *   void getFlow(cv::Mat prev, cv::Mat next, cv::Mat& u, cv::Mat& v) :43-75
+ *
+ * Its FFI surface is therefore C++/cv::Mat; the functions below are the
+ * plain-pointer entry points that surface lowers onto (include/hornSchunck.hpp
+ * is the cv::Mat adapter with the reference's exact signatures; INTEGRATION.md
+ * shows the binding).  No torch or OpenCV types cross this boundary.
+ *
+ * Semantics (identical to the reference, computed in fp32 on the GPU):
+ *   Ix, Iy = 3x3 Sobel of I0 (reflect-101 border), It = I1 - I0;
+ *   u = v = 0; repeat `iters` times:
+ *     ubar, vbar = windowSize x windowSize box mean (zero border, anchor
+ *                  windowSize - windowSize/2 - 1)
+ *     c = (Ix ubar + Iy vbar + It) / (alpha^2 + Ix^2 + Iy^2)
+ *     u = ubar - Ix c;  v = vbar - Iy c
+ * Parity: max|u - u_ref| / max|u_ref| <= 1e-4 against the float64 reference.
+ *
+ * Threading: a context is used by one host thread at a time.  Host-buffer
+ * calls are blocking (as the reference is).  *_device calls are
+ * stream-ordered, never synchronise the host and never allocate, so they may
+ * be captured into a hipGraph.
+ */
+#ifndef HSFLOW_H
+#define HSFLOW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HSFLOW_VERSION 10000 /* 1.0.0 */
+
+/* Status codes (0 ok, <0 error).  The reference has no codes: OpenCV throws
+ * cv::Exception (e.g. size mismatch in multiply, hornSchunck.cpp:63-70);
+ * the cv::Mat adapter maps every non-zero status to an exception. */
+enum {
+    HSFLOW_OK = 0,
+    HSFLOW_ERR_ARG = -1,   /* null pointer, bad size/window/dtype/stride     */
+    HSFLOW_ERR_HIP = -2,   /* HIP runtime error; see hsflow_last_error()      */
+    HSFLOW_ERR_OOM = -3,   /* device allocation failed                        */
+    HSFLOW_ERR_NODEV = -4, /* no HIP device / device index out of range       */
+    HSFLOW_ERR_SIZE = -5   /* prev/next sizes differ (main.cpp:71-73)         */
+};
+
+/* Element types.  U8 = CV_8UC1, F32 = CV_32FC1, F64 = CV_64FC1. */
+enum { HSFLOW_U8 = 0, HSFLOW_F32 = 1, HSFLOW_F64 = 2 };
+
+/* Largest windowSize accepted (hornSchunck.cpp:53 allows any; OpenCV would
+ * take a few seconds per iteration at this size already). */
+#define HSFLOW_MAX_WINDOW 63
+
+typedef struct hsflow_ctx hsflow_ctx;
+
+int hsflow_version(void);
+const char *hsflow_status_string(int status);
+
+/* Context = device + stream + cached device buffers (grow-only). */
+int hsflow_create(hsflow_ctx **ctx, int device);
+void hsflow_destroy(hsflow_ctx *ctx);
+const char *hsflow_last_error(const hsflow_ctx *ctx);
+/* The HIP stream the host-buffer calls run on (hipStream_t as void*). */
+void *hsflow_stream(hsflow_ctx *ctx);
+
+/* ---- host-buffer, blocking: the reference's two methods ---------------- */
+
+/* hornSchunck::getFlow (hornSchunck.cpp:43-75).  I0/I1: rows x cols, element
+ * type dtype_in, row step in BYTES (cv::Mat::step; non-continuous ROIs ok).
+ * u/v: rows x cols of dtype_out (HSFLOW_F64 = what the reference returns,
+ * CV_64FC1, or HSFLOW_F32), row step out_step bytes. */
+int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
+                int rows, int cols, size_t in_step, int window, int iters,
+                double alpha, void *u, void *v, int dtype_out, size_t out_step);
+
+/* hornSchunck::getGradients (hornSchunck.cpp:19-41): gx, gy, gt. */
+int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
+                     int rows, int cols, size_t in_step, void *gx, void *gy,
+                     void *gt, int dtype_out, size_t out_step);
+
+/* ---- device pointers, stream-ordered ------------------------------------
+ * A batch is `batch` independent frame pairs stored back to back:
+ * I0[b][rows][cols], dense (pitch = cols elements), likewise u, v.
+ * Inputs are U8 or F32.  Outputs are f32.  `stream` is a hipStream_t (NULL =
+ * default stream).  `workspace` is device memory of at least
+ * hsflow_workspace_bytes(rows, cols, batch) bytes, 256-byte aligned. */
+size_t hsflow_workspace_bytes(int rows, int cols, int batch);
+
+/* Full solve: gradients + `iters` Jacobi iterations from u = v = 0. */
+int hsflow_flow_device(const void *I0, const void *I1, int dtype_in, int rows,
+                       int cols, int batch, int window, int iters, float alpha,
+                       float *u, float *v, void *workspace, size_t workspace_bytes,
+                       void *stream);
+
+/* The two phases separately (bench / profiling / warm starts):
+ * gradients into the workspace (optionally also to gx/gy/gt, may be NULL)... */
+int hsflow_gradients_device(const void *I0, const void *I1, int dtype_in, int rows,
+                            int cols, int batch, float *gx, float *gy, float *gt,
+                            void *workspace, size_t workspace_bytes, void *stream);
+/* ...then `iters` Jacobi iterations from the gradients in the workspace,
+ * starting from (u, v) when warm_start != 0, else from zero. */
+int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
+                         float alpha, int warm_start, float *u, float *v,
+                         void *workspace, size_t workspace_bytes, void *stream);
+
+/* Iterations fused per Jacobi launch (temporal blocking depth) the library
+ * picks for this shape; 0 = automatic (default).  Results are bit-identical
+ * for every depth.  Process-wide; not thread-safe against running solves. */
+int hsflow_set_iters_per_launch(int k);
+int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
+
+/* ---- host utilities on the path to the hot loop ------------------------ */
+
+/* main.cpp:13-14 cv::cvtColor(BGR2GRAY) for 8-bit BGR, OpenCV 4.x 15-bit
+ * fixed point: Y = (9798 R + 19235 G + 3735 B + 16384) >> 15. */
+int hsflow_bgr_to_gray(const uint8_t *bgr, int rows, int cols, size_t bgr_step,
+                       uint8_t *gray, size_t gray_step);
+
+/* Deterministic synthetic frame pair: I0 = smoothed hash noise
+ * around 128 (integer-valued 0..255), I1 = I0's texture shifted by
+ * (dy, dx) = (qdy/4, qdx/4) px with integer bilinear weights.  Outputs are
+ * rows x cols f32 (dense) and/or u8 (either pointer may be NULL). */
+int hsflow_synth_pair(uint64_t seed, int rows, int cols, int qdy, int qdx,
+                      float *I0, float *I1, uint8_t *I0_u8, uint8_t *I1_u8);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HSFLOW_H */

@@ -1,0 +1,96 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol declared in
+include/hsflow.h, validates arguments, and its host utilities are exact.
+No GPU compute here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import hsflow
+from conftest import GOLDEN, ROOT
+from synth_ref import synth_pair as np_synth
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "hsflow.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(hsflow_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = hsflow.lib()
+    syms = header_symbols()
+    assert len(syms) >= 16
+    for s in syms:
+        assert hasattr(L, s), f"libhsflow.so lacks {s}"
+    assert sorted(hsflow.EXPORTS) == syms
+
+
+def test_version_and_status_strings():
+    L = hsflow.lib()
+    assert L.hsflow_version() == 10000
+    assert L.hsflow_status_string(0) == b"ok"
+    assert L.hsflow_status_string(-5) == b"image sizes differ"
+
+
+def test_workspace_bytes():
+    n = hsflow.workspace_bytes(1080, 1920, 2)
+    assert n >= 1080 * 1920 * 2 * 24
+    assert hsflow.workspace_bytes(0, 10, 1) == 0
+    assert hsflow.workspace_bytes(10, 10, 0) == 0
+
+
+def test_iters_per_launch_policy():
+    assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 4
+    assert hsflow.iters_per_launch(1080, 1920, 1, 3) == 8
+    assert hsflow.iters_per_launch(1080, 1920, 1, 12) == 1
+    with pytest.raises(hsflow.HsflowError):
+        hsflow.set_iters_per_launch(-1)
+    hsflow.set_iters_per_launch(2)
+    assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 2
+    hsflow.set_iters_per_launch(0)
+
+
+def test_device_entry_points_validate_before_touching_the_gpu():
+    L = hsflow.lib()
+    # bad sizes / null pointers are rejected without any HIP call
+    assert L.hsflow_flow_device(None, None, 1, 0, 10, 1, 5, 10, 1.0, None, None,
+                                None, 0, None) == hsflow.HSFLOW_ERR_ARG
+    assert L.hsflow_jacobi_device(10, 10, 1, 0, 1, 1.0, 0, 1, 1, 1, 10 ** 6,
+                                  None) == hsflow.HSFLOW_ERR_ARG
+    assert L.hsflow_jacobi_device(10, 10, 1, 5, 1, 1.0, 0, 1, 1, 1, 16,
+                                  None) == hsflow.HSFLOW_ERR_ARG  # workspace too small
+    assert L.hsflow_gradients_device(1, 1, 2, 10, 10, 1, None, None, None, 1, 10 ** 6,
+                                     None) == hsflow.HSFLOW_ERR_ARG  # F64 on device
+
+
+def test_host_api_rejects_null_context():
+    L = hsflow.lib()
+    assert L.hsflow_flow(None, 1, 1, 0, 4, 4, 4, 5, 1, 1.0, 1, 1, 2, 32) == hsflow.HSFLOW_ERR_ARG
+
+
+def test_bgr_to_gray_matches_reference_conversion():
+    z = np.load(os.path.join(GOLDEN, "bgr_crop.npz"))
+    assert np.array_equal(hsflow.bgr_to_gray(z["bgr"]), z["gray"])
+
+
+@pytest.mark.parametrize("rows,cols,qdy,qdx", [(37, 53, -3, 6), (16, 16, 0, 0),
+                                               (64, 40, 5, -7), (1, 1, -3, 6)])
+def test_synth_pair_matches_numpy_twin(rows, cols, qdy, qdx):
+    a0, a1 = hsflow.synth_pair(1000, rows, cols, qdy, qdx)
+    b0, b1 = np_synth(1000, rows, cols, qdy, qdx)
+    assert np.array_equal(a0, b0) and np.array_equal(a1, b1)
+    u0, u1 = hsflow.synth_pair(1000, rows, cols, qdy, qdx, dtype=np.uint8)
+    assert np.array_equal(u0.astype(np.float32), a0)
+
+
+def test_synth_pair_statistics():
+    I0, I1 = hsflow.synth_pair(1000, 256, 256)
+    assert I0.min() >= 0 and I0.max() <= 255
+    assert 25 < I0.std() < 55 and abs(I0.mean() - 128) < 8
+    # I1 is I0 moved by (+1.5 cols, -0.75 rows): I1[r, c] ~ I0[r+0.75, c-1.5]
+    err = np.abs(I1[10:-10, 10:-10] - 0.5 * (I0[11:-9, 8:-12] + I0[11:-9, 9:-11]))
+    assert err.mean() < 6
+    c0, c1 = hsflow.synth_pair(1001, 64, 64)
+    assert not np.array_equal(c0, I0[:64, :64])

@@ -1,0 +1,259 @@
+"""GPU parity tests: the HIP path (libhsflow.so, through its C ABI) against the
+CPU float64 oracle (oracle/hs_oracle.c) and the golden fixtures.
+
+Tolerance (north_star: "within 1e-4 relative fp32"; SURVEY §8c form):
+    max|got - ref| / max|ref| <= 1e-4        (TOL below)
+Integer work (gradients, packing, plot KAT label maps, K-invariance, batch
+vs single) is checked bit-exactly.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import kat_labels, norm_rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def hs():
+    import hsflow
+    return hsflow
+
+
+@pytest.fixture(scope="module")
+def ctx(hs):
+    c = hs.Context(0)
+    yield c
+    c.close()
+
+
+def _oracle_flow(I0, I1, w, n, alpha=1.0):
+    return oracle.flow(I0, I1, w, n, alpha, nthreads=8)
+
+
+def test_native_library_is_loaded(hs, ctx):
+    with open("/proc/self/maps") as f:
+        maps = f.read()
+    assert "libhsflow.so" in maps
+
+
+@pytest.mark.parametrize("w,n", [(5, 1), (5, 10), (5, 100), (3, 1), (3, 10), (3, 100),
+                                 (4, 10), (1, 10), (2, 10), (7, 10), (9, 10)])
+def test_crop_matches_golden(hs, ctx, crop_small, w, n):
+    u, v = ctx.flow(crop_small["I0"], crop_small["I1"], w, n, 1.0)
+    assert u.dtype == np.float64  # CV_64FC1 like the reference
+    assert norm_rel_err(u, crop_small[f"u_w{w}_n{n}"]) <= TOL
+    assert norm_rel_err(v, crop_small[f"v_w{w}_n{n}"]) <= TOL
+
+
+def test_alpha(hs, ctx, crop_small):
+    u, v = ctx.flow(crop_small["I0"], crop_small["I1"], 5, 10, 15.0)
+    assert norm_rel_err(u, crop_small["u_w5_n10_a15"]) <= TOL
+    assert norm_rel_err(v, crop_small["v_w5_n10_a15"]) <= TOL
+
+
+def test_config1_crop256(hs, crop256):
+    """BASELINE config 1: KITTI 000050 centre crop, ws 5, alpha 1, 100 it."""
+    u, v = hs.hornSchunck(5, 100, 1.0).getFlow(crop256["I0"], crop256["I1"])
+    assert norm_rel_err(u, crop256["u"]) <= TOL
+    assert norm_rel_err(v, crop256["v"]) <= TOL
+
+
+@pytest.mark.parametrize("tag", ["000050", "000040"])
+def test_reference_plot_kat(hs, kitti, golden_meta, tag):
+    """The reference's own arrow plot (main.cpp:94-104 -> plotFlow.cpp:68-88)
+    is reproduced pixel-exactly from the GPU (u, v)."""
+    I0, I1 = kitti[tag]
+    hsobj = hs.hornSchunck(5, 100, 1.0)
+    u, v = hsobj.getFlow(I0, I1)
+    uo, vo = _oracle_flow(I0, I1, 5, 100)
+    assert norm_rel_err(u, uo) <= TOL and norm_rel_err(v, vo) <= TOL
+    meta = golden_meta["kat"][tag]
+    assert abs(u.sum() - meta["sum_u"]) <= 1e-4 * abs(meta["sum_u"])
+    assert abs(v.sum() - meta["sum_v"]) <= 1e-4 * abs(meta["sum_v"])
+    canvas = np.zeros(I0.shape + (3,), np.uint8)
+    img = oracle.plot_bresenham(canvas, u, v, 20, 20.0, 5)
+    lab = np.zeros(I0.shape, np.uint8)
+    lab[(img[..., 0] == 0) & (img[..., 1] == 255) & (img[..., 2] == 0)] = 1
+    lab[(img[..., 0] == 0) & (img[..., 1] == 0) & (img[..., 2] == 255)] = 2
+    ref, amb = kat_labels(tag)
+    assert int(np.count_nonzero((lab != ref) & ~amb)) == 0
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.float32, np.float64])
+def test_gradients_exact(hs, ctx, kitti, dtype):
+    I0, I1 = kitti["000050"]
+    gx, gy, gt = ctx.gradients(I0.astype(dtype), I1.astype(dtype))
+    ex, ey, et = oracle.gradients(I0, I1)
+    assert np.array_equal(gx, ex) and np.array_equal(gy, ey) and np.array_equal(gt, et)
+
+
+def test_get_gradients_mirror(hs, crop_small):
+    gx, gy, gt = hs.hornSchunck(5, 1, 1.0).getGradients(crop_small["I0"], crop_small["I1"])
+    assert np.array_equal(gx, crop_small["gx"]) and np.array_equal(gt, crop_small["gt"])
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 7), (7, 1), (2, 2), (3, 130), (130, 3),
+                                   (47, 63), (65, 65), (49, 300), (300, 49), (97, 129)])
+@pytest.mark.parametrize("w", [3, 5])
+def test_ragged_and_tiny_shapes(hs, ctx, shape, w):
+    I0, I1 = hs.synth_pair(1234, *shape, dtype=np.uint8)
+    u, v = ctx.flow(I0, I1, w, 13, 1.0)
+    uo, vo = _oracle_flow(I0, I1, w, 13)
+    if np.abs(uo).max() == 0:
+        assert np.abs(u).max() == 0
+    else:
+        assert norm_rel_err(u, uo) <= TOL and norm_rel_err(v, vo) <= TOL
+
+
+@pytest.mark.parametrize("w", [1, 2, 4, 6, 8, 10, 11, 15, 21])
+def test_all_window_sizes(hs, ctx, w):
+    I0, I1 = hs.synth_pair(77, 45, 70, dtype=np.uint8)
+    u, v = ctx.flow(I0, I1, w, 7, 1.0)
+    uo, vo = _oracle_flow(I0, I1, w, 7)
+    assert norm_rel_err(u, uo) <= TOL and norm_rel_err(v, vo) <= TOL
+
+
+def test_zero_iterations_gives_zero_flow(hs, ctx, crop_small):
+    u, v = ctx.flow(crop_small["I0"], crop_small["I1"], 5, 0, 1.0)
+    assert not u.any() and not v.any()
+
+
+def test_non_integral_f32_inputs_use_f32_gradients(hs, ctx):
+    I0, I1 = hs.synth_pair(5, 150, 170)
+    rng = np.random.default_rng(0)
+    I0 = (I0 + rng.uniform(-0.5, 0.5, I0.shape)).astype(np.float32)
+    I1 = (I1 * 0.731).astype(np.float32)
+    for w, n in [(5, 40), (3, 40), (7, 9)]:
+        u, v = ctx.flow(I0, I1, w, n, 1.0)
+        uo, vo = _oracle_flow(I0.astype(np.float64), I1.astype(np.float64), w, n)
+        assert norm_rel_err(u, uo) <= TOL and norm_rel_err(v, vo) <= TOL
+
+
+def test_roi_input_honours_row_step(hs, ctx, kitti):
+    """cv::Mat ROIs are non-continuous (hornSchunck.cpp takes Mat by value)."""
+    I0, I1 = kitti["000040"]
+    roi0, roi1 = I0[30:130, 100:333], I1[30:130, 100:333]
+    assert not roi0.flags["C_CONTIGUOUS"]
+    u, v = ctx.flow(roi0, roi1, 5, 20, 1.0)
+    u2, v2 = ctx.flow(np.ascontiguousarray(roi0), np.ascontiguousarray(roi1), 5, 20, 1.0)
+    assert np.array_equal(u, u2) and np.array_equal(v, v2)
+
+
+def test_size_mismatch_raises(hs, ctx):
+    with pytest.raises(hs.HsflowError) as e:
+        ctx.flow(np.zeros((4, 4), np.uint8), np.zeros((4, 5), np.uint8), 5, 1, 1.0)
+    assert e.value.status == hs.HSFLOW_ERR_SIZE
+
+
+def test_f32_output(hs, ctx, crop_small):
+    u32, _ = ctx.flow(crop_small["I0"], crop_small["I1"], 5, 10, 1.0, out_dtype=np.float32)
+    u64, _ = ctx.flow(crop_small["I0"], crop_small["I1"], 5, 10, 1.0)
+    assert u32.dtype == np.float32 and np.array_equal(u32.astype(np.float64), u64)
+
+
+# --------------------------------------------------------------- invariances
+def _device_flow(hs, I0, I1, w, n, kb):
+    import torch
+    hs.set_iters_per_launch(kb)
+    try:
+        u, v = hs.flow_device(I0, I1, w, n, 1.0)
+        torch.cuda.synchronize()
+    finally:
+        hs.set_iters_per_launch(0)
+    return u.cpu().numpy(), v.cpu().numpy()
+
+
+@pytest.mark.parametrize("dtype", ["uint8", "float32"])
+def test_blocking_depth_is_bit_invariant(hs, dtype):
+    """Temporal blocking (KB iterations per launch) changes no bit."""
+    import torch
+    I0, I1 = hs.synth_pair(1001, 300, 517, dtype=np.uint8)
+    t0 = torch.from_numpy(I0.astype(dtype)).cuda()
+    t1 = torch.from_numpy(I1.astype(dtype)).cuda()
+    ref = _device_flow(hs, t0, t1, 5, 23, 1)
+    for kb in (2, 4, 8):
+        got = _device_flow(hs, t0, t1, 5, 23, kb)
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), kb
+    ref3 = _device_flow(hs, t0, t1, 3, 19, 1)
+    for kb in (2, 4, 8):
+        got = _device_flow(hs, t0, t1, 3, 19, kb)
+        assert np.array_equal(got[0], ref3[0]), kb
+
+
+def test_blocking_depth_bit_invariant_f32_gradients(hs):
+    import torch
+    I0, I1 = hs.synth_pair(9, 200, 333)
+    I0 = I0 + np.float32(0.25)
+    t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
+    ref = _device_flow(hs, t0, t1, 5, 11, 1)
+    for kb in (2, 4):
+        got = _device_flow(hs, t0, t1, 5, 11, kb)
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+
+
+def test_batch_equals_single_pairs(hs, ctx):
+    import torch
+    pairs = [hs.synth_pair(1000 + i, 130, 250) for i in range(3)]
+    b0 = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    b1 = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    # pair 1 made non-integral: the batch mixes both gradient formats
+    b0[1] += 0.5
+    u, v = hs.flow_device(b0, b1, 5, 30, 1.0)
+    torch.cuda.synchronize()
+    for i in range(3):
+        us, vs = hs.flow_device(b0[i].contiguous(), b1[i].contiguous(), 5, 30, 1.0)
+        torch.cuda.synchronize()
+        assert torch.equal(u[i], us) and torch.equal(v[i], vs)
+        uo, vo = _oracle_flow(b0[i].cpu().numpy(), b1[i].cpu().numpy(), 5, 30)
+        assert norm_rel_err(u[i].cpu().numpy(), uo) <= TOL
+
+
+def test_warm_start_continuation_is_exact(hs):
+    import torch
+    I0, I1 = hs.synth_pair(3, 240, 320)
+    t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
+    u10, v10 = hs.flow_device(t0, t1, 5, 10, 1.0)
+    ws = hs.alloc_workspace(240, 320)
+    hs.gradients_device(t0, t1, ws)
+    u = torch.empty_like(t0)
+    v = torch.empty_like(t0)
+    hs.jacobi_device(240, 320, 1, 5, 4, 1.0, u, v, ws)
+    hs.jacobi_device(240, 320, 1, 5, 6, 1.0, u, v, ws, warm_start=True)
+    torch.cuda.synchronize()
+    assert torch.equal(u, u10) and torch.equal(v, v10)
+
+
+# ------------------------------------------------------- full-size (configs)
+def test_1080p_against_oracle(hs):
+    """Config 2 shape (1920x1080 f32 synthetic), 30 iterations vs the oracle."""
+    import torch
+    I0, I1 = hs.synth_pair(1000, 1080, 1920)
+    u, v = hs.flow_device(torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda(),
+                          5, 30, 1.0)
+    uo, vo = _oracle_flow(I0, I1, 5, 30)
+    assert norm_rel_err(u.cpu().numpy(), uo) <= TOL
+    assert norm_rel_err(v.cpu().numpy(), vo) <= TOL
+    # Sobel scaling: the mean flow is ~dx/8 = 0.1875 (SURVEY §8d sanity)
+    assert 0.05 < float(u.mean()) < 0.3
+
+
+def test_4k_500_properties(hs):
+    """Config 3 shape at full iteration count: size-independent properties
+    (KB invariance, batch==single, finite, expected mean motion)."""
+    import torch
+    I0, I1 = hs.synth_pair(1000, 2160, 3840)
+    t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
+    a = _device_flow(hs, t0, t1, 5, 500, 4)
+    b = _device_flow(hs, t0, t1, 5, 500, 2)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert np.isfinite(a[0]).all() and np.isfinite(a[1]).all()
+    assert 0.05 < float(a[0].mean()) < 0.3
+    # oracle check on a corner of the same frame (short run)
+    s0, s1 = I0[:512, :768].copy(), I1[:512, :768].copy()
+    us, _ = _device_flow(hs, torch.from_numpy(s0).cuda(), torch.from_numpy(s1).cuda(), 5, 40, 4)
+    uo, _ = _oracle_flow(s0, s1, 5, 40)
+    assert norm_rel_err(us, uo) <= TOL
