@@ -1,0 +1,212 @@
+"""Horn-Schunck throughput bench (BASELINE.json metric: Mpix*iter/s + pairs/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1080p|4k]
+
+One step = one full solve (K1 gradients + `iters` Jacobi iterations, the
+reference's getFlow, hornSchunck.cpp:43-75) of a batch of synthetic frame
+pairs per GPU, inputs already resident in HBM.  Frame pairs are independent,
+so for N > 1 each rank (one process per GPU, torch.distributed over RCCL)
+solves its own pairs: weak scaling, no data-path collective (the timing
+barrier and max-over-ranks reduction are the only collectives).
+
+Rank 0 prints ONE JSON line.  Besides the driver fields it carries
+  roofline      dominant kernel (K2, hs_jacobi_kernel) measured live with
+                events on the launch stream; algorithmic bytes per launch are
+                the compulsory HBM bytes of one temporally-blocked pass
+                (DESIGN.md "Roofline"), traffic = PMC-measured bytes from the
+                committed rocprofv3 summary under profiles/ (or null)
+  cpu_baseline  the float64 CPU port (oracle/, mirrors hornSchunck.cpp pass
+                by pass) on a bounded sample, 1 thread, rank 0 only
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cpp-optical-flow_amd"))
+
+WORKLOADS = {
+    # BASELINE.json configs[1] / configs[2]
+    "1080p": dict(rows=1080, cols=1920, iters=300, batch=8),
+    "4k": dict(rows=2160, cols=3840, iters=500, batch=2),
+}
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p")
+    ap.add_argument("--batch", type=int, default=0, help="pairs per GPU per step")
+    ap.add_argument("--iters", type=int, default=0)
+    ap.add_argument("--window", type=int, default=5)
+    ap.add_argument("--alpha", type=float, default=1.0)
+    ap.add_argument("--dtype", choices=["f32", "u8"], default="f32",
+                    help="input frame element type (configs use f32)")
+    ap.add_argument("--kb", type=int, default=0, help="iterations per K2 launch (0 auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=0,
+                    help="Jacobi iterations of the CPU sample (0: auto ~15 s)")
+    ap.add_argument("--roofline-reps", type=int, default=3)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import hsflow
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    wl = dict(WORKLOADS[args.workload])
+    rows, cols = wl["rows"], wl["cols"]
+    iters = args.iters or wl["iters"]
+    batch = args.batch or wl["batch"]
+    if args.kb:
+        hsflow.set_iters_per_launch(args.kb)
+
+    # synthetic pairs, seed 1000 + global pair index
+    np_dtype = np.float32 if args.dtype == "f32" else np.uint8
+    pairs = [hsflow.synth_pair(1000 + rank * batch + i, rows, cols, dtype=np_dtype)
+             for i in range(batch)]
+    I0 = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
+    I1 = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
+    del pairs
+    u = torch.empty((batch, rows, cols), dtype=torch.float32, device=dev)
+    v = torch.empty_like(u)
+    ws = hsflow.alloc_workspace(rows, cols, batch, dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        hsflow.flow_device(I0, I1, args.window, iters, args.alpha, u, v, ws, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+
+    px = rows * cols
+    total_pairs = batch * world * args.steps
+    value = total_pairs * px * iters / elapsed / 1e6
+    ok = bool(torch.isfinite(u).all().item()) and 0.05 < float(u.mean()) < 0.3
+
+    # ---- dominant-kernel roofline: K2 alone, events on the launch stream --
+    kb = hsflow.iters_per_launch(rows, cols, batch, args.window) if not args.kb else args.kb
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    hsflow.gradients_device(I0, I1, ws, stream=stream)
+    launches_per_solve = -(-iters // kb)
+    reps = args.roofline_reps
+    torch.cuda.synchronize(dev)
+    ev0.record(stream)
+    for _ in range(reps):
+        hsflow.jacobi_device(rows, cols, batch, args.window, iters, args.alpha, u, v, ws,
+                             stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    k2_ms = ev0.elapsed_time(ev1) / (reps * launches_per_solve)
+    n_px = batch * px
+    # compulsory bytes of one blocked pass: read u, v (f32) + packed gradients
+    # (4 B) + write u, v; the first pass of a solve reads no u, v
+    first_frac = 1.0 / launches_per_solve
+    bytes_per_launch = n_px * (8 + 4 + 8 - 8 * first_frac)
+    achieved = bytes_per_launch / (k2_ms * 1e-3) / 1e9
+    jacobi_equiv = 28.0 * n_px * kb / (k2_ms * 1e-3) / 1e9  # SURVEY §8d 28 B/px*iter
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        if pmc.get("kb") == kb and pmc.get("batch") == batch:
+            traffic = pmc.get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(rows, cols, args.window, args.alpha, args.cpu_iters)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpix*iter/s (Horn-Schunck Jacobi) + frame-pairs/s",
+            "value": round(value, 1),
+            "unit": "Mpix*iter/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic {args.dtype} frame pairs (hash texture, shift (-0.75,+1.5) px)",
+            "config": {"workload": f"{args.workload} {cols}x{rows}, {iters} it, ws {args.window}",
+                       "rows": rows, "cols": cols, "iters": iters, "window": args.window,
+                       "alpha": args.alpha, "pairs_per_gpu_per_step": batch,
+                       "iters_per_launch": kb, "parallelism": f"frame-parallel x{world}"},
+            "pairs_per_s": round(total_pairs / elapsed, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel": "hs_jacobi_kernel",
+                         "avg_launch_ms": round(k2_ms, 5),
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                         "jacobi_equiv_GBps_28B": round(jacobi_equiv, 1)},
+            "cpu_baseline": cpu,
+            "sane": ok,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(rows, cols, window, alpha, cpu_iters):
+    """oracle/ float64 port of hornSchunck.cpp (pass-per-OpenCV-call, fresh
+    temporaries each iteration), 1 thread, on the same synthetic pair at full
+    size for a bounded number of iterations."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import hsflow
+    I0, I1 = hsflow.synth_pair(1000, rows, cols)
+    if not cpu_iters:
+        t = time.perf_counter()
+        oracle.flow(I0, I1, window, 1, alpha, nthreads=1)
+        one = time.perf_counter() - t
+        cpu_iters = max(1, min(60, int(15.0 / max(one, 1e-3))))
+    t = time.perf_counter()
+    oracle.flow(I0, I1, window, cpu_iters, alpha, nthreads=1)
+    dt = time.perf_counter() - t
+    return {"value": round(rows * cols * cpu_iters / dt / 1e6, 2), "unit": "Mpix*iter/s",
+            "cores": 1, "kind": "port",
+            "sample": f"{cols}x{rows} pair, {cpu_iters} Jacobi iterations incl. gradients, "
+                      f"float64, {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

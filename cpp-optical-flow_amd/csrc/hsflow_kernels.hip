@@ -42,9 +42,11 @@ __device__ __forceinline__ uint32_t pack_grad(int ix, int iy, int it) {
 }
 __device__ __forceinline__ void unpack_grad(uint32_t p, float &ix, float &iy,
                                             float &it) {
-    ix = (float)__builtin_amdgcn_sbfe(p, 0, 11);
-    iy = (float)__builtin_amdgcn_sbfe(p, 11, 11);
-    it = (float)__builtin_amdgcn_sbfe(p, 22, 9);
+    // v_bfe_i32 sign-extends; the builtin is typed unsigned, so cast back to
+    // int before converting (else v_cvt_f32_u32 turns -1 into 4.29e9)
+    ix = (float)(int)__builtin_amdgcn_sbfe(p, 0, 11);
+    iy = (float)(int)__builtin_amdgcn_sbfe(p, 11, 11);
+    it = (float)(int)__builtin_amdgcn_sbfe(p, 22, 9);
 }
 
 __device__ __forceinline__ int reflect101(int p, int len) {
@@ -183,14 +185,14 @@ __device__ __forceinline__ void jacobi_region(const JacobiArgs &p, size_t pbase,
         for (int r = 0; r < RH; ++r) {
             const bool in = col_in && ((rowmask >> r) & 1ull);
             const int off = in ? off0 + r * cols * 4 : kOOB;
-            u[r] = __builtin_amdgcn_raw_buffer_load_b32(u_rs, off, 0, 0);
-            v[r] = __builtin_amdgcn_raw_buffer_load_b32(v_rs, off, 0, 0);
+            u[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, off, 0, 0));
+            v[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, off, 0, 0));
             if constexpr (PACKED) {
                 g[r] = __builtin_amdgcn_raw_buffer_load_b32(g_rs, off, 0, 0);
             } else {
-                gxr[r] = __builtin_amdgcn_raw_buffer_load_b32(gx_rs, off, 0, 0);
-                gyr[r] = __builtin_amdgcn_raw_buffer_load_b32(gy_rs, off, 0, 0);
-                gtr[r] = __builtin_amdgcn_raw_buffer_load_b32(gt_rs, off, 0, 0);
+                gxr[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gx_rs, off, 0, 0));
+                gyr[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gy_rs, off, 0, 0));
+                gtr[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gt_rs, off, 0, 0));
             }
         }
     }
@@ -247,8 +249,8 @@ __device__ __forceinline__ void jacobi_region(const JacobiArgs &p, size_t pbase,
         for (int r = HL; r < RH - HR; ++r) {
             const bool in = st_lane && (r - HL) < nout && ((rowmask >> r) & 1ull);
             const int off = in ? off0 + (r - HL) * cols * 4 : kOOB;
-            __builtin_amdgcn_raw_buffer_store_b32(u[r], uo_rs, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(v[r], vo_rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(u[r]), uo_rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), vo_rs, off, 0, 0);
         }
     }
 }
