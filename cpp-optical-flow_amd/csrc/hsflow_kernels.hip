@@ -99,25 +99,70 @@ __global__ __launch_bounds__(256) void hs_gradients_kernel(
 }
 
 // ----------------------------------------------------------------------- K2
-// value of x held by lane (lane + D) of this wavefront (wraps at 64; callers
-// only use wrapped results in the invalid halo)
-template <int D> __device__ __forceinline__ float lane_rel(float x, int lane) {
-    if constexpr (D == 0) {
-        return x;
+// Cross-lane shifts by one lane over the whole wavefront: DPP wave_shr:1 /
+// wave_shl:1 (GFX9-family DPP, kept on gfx950).  They fuse into the consuming
+// v_add_f32 as a DPP source modifier: pure VALU, no LDS crossbar traffic.
+// Lanes shifted in from outside the wave read 0 (bound_ctrl); those results
+// only ever land in the region's halo columns, which are never stored.
+__device__ __forceinline__ float from_left(float x) {  // lane l <- lane l-1
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x138, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float from_right(float x) {  // lane l <- lane l+1
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x130, 0xF, 0xF, true));
+}
+
+// Horizontal window sum over lanes [l - A, l + W-1-A] (A = anchor).  The
+// summation order is fixed per W, so every blocking depth gives the same bits.
+template <int W> __device__ __forceinline__ float hsum(float x);
+
+// Two independent fields (u and v) in lockstep, statement by statement, so
+// each DPP read of a just-written VGPR has the other field's instruction as
+// its wait state instead of an s_nop.
+template <int W>
+__device__ __forceinline__ void hsum2(float x, float y, float &hx, float &hy) {
+    if constexpr (W == 5) {
+        const float ax = from_left(x) + x;
+        const float ay = from_left(y) + y;
+        const float bx = from_left(ax) + from_right(ax);
+        const float by = from_left(ay) + from_right(ay);
+        const float cx = from_right(x);
+        const float cy = from_right(y);
+        hx = bx + from_right(cx);
+        hy = by + from_right(cy);
+    } else if constexpr (W == 3) {
+        const float ax = from_left(x) + x;
+        const float ay = from_left(y) + y;
+        hx = ax + from_right(x);
+        hy = ay + from_right(y);
     } else {
-        return __int_as_float(
-            __builtin_amdgcn_ds_bpermute(((lane + D) & 63) << 2, __float_as_int(x)));
+        hx = hsum<W>(x);
+        hy = hsum<W>(y);
     }
 }
 
-template <int W, int D = -(W - W / 2 - 1)>
-__device__ __forceinline__ float hsum(float x, int lane) {
-    // sum over lanes lane-A .. lane+W-1-A, left to right (A = anchor)
-    constexpr int A = W - W / 2 - 1;
-    if constexpr (D == W - 1 - A) {
-        return lane_rel<D>(x, lane);
+template <int W> __device__ __forceinline__ float hsum(float x) {
+    constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
+    if constexpr (W == 1) {
+        return x;
+    } else if constexpr (W == 3) {
+        return (from_left(x) + x) + from_right(x);
+    } else if constexpr (W == 5) {
+        // a(l) = x(l-1) + x(l);  hs = (a(l-1) + a(l+1)) + x(l+2)
+        const float a = from_left(x) + x;
+        return (from_left(a) + from_right(a)) + from_right(from_right(x));
     } else {
-        return lane_rel<D>(x, lane) + hsum<W, D + 1>(x, lane);
+        float s = x, m = x, r = x;
+#pragma unroll
+        for (int d = 0; d < A; ++d) {
+            m = from_left(m);
+            s += m;
+        }
+#pragma unroll
+        for (int d = 0; d < AR; ++d) {
+            r = from_right(r);
+            s += r;
+        }
+        return s;
     }
 }
 
@@ -199,18 +244,33 @@ __device__ __forceinline__ void jacobi_region(const JacobiArgs &p, size_t pbase,
 
     const float alpha2 = p.alpha2, inv = p.inv_w2;
     for (int it = 0; it < p.iters; ++it) {
-        float ru[W], rv[W];  // ring of horizontal sums, compile-time indexed
+        // rings of horizontal sums (hu, hv) and, for W = 5, of vertical pair
+        // sums q(y) = h(y) + h(y+1); all indices are compile-time
+        float hu[W], hv[W], qu[W], qv[W];
 #pragma unroll
         for (int r = 0; r < RH; ++r) {
-            ru[r % W] = hsum<W>(u[r], lane);
-            rv[r % W] = hsum<W>(v[r], lane);
+            hsum2<W>(u[r], v[r], hu[r % W], hv[r % W]);
+            if constexpr (W == 5) {
+                if (r >= 1) {
+                    qu[(r - 1) % W] = hu[(r - 1) % W] + hu[r % W];
+                    qv[(r - 1) % W] = hv[(r - 1) % W] + hv[r % W];
+                }
+            }
             const int y = r - AR;  // output row whose window ends at row r
             if (y >= A) {
-                float su = 0.f, sv = 0.f;
+                float su, sv;
+                if constexpr (W == 5) {
+                    // (h(y-2) + h(y-1)) + (h(y) + h(y+1)) + h(y+2)
+                    su = (qu[(y - 2) % W] + qu[y % W]) + hu[(y + 2) % W];
+                    sv = (qv[(y - 2) % W] + qv[y % W]) + hv[(y + 2) % W];
+                } else {
+                    su = hu[(y - A) % W];
+                    sv = hv[(y - A) % W];
 #pragma unroll
-                for (int d = 0; d < W; ++d) {
-                    su += ru[(y - A + d) % W];
-                    sv += rv[(y - A + d) % W];
+                    for (int d = 1; d < W; ++d) {
+                        su += hu[(y - A + d) % W];
+                        sv += hv[(y - A + d) % W];
+                    }
                 }
                 const float ub = su * inv, vb = sv * inv;
                 float ix, iy, itv;

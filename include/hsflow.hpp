@@ -1,0 +1,158 @@
+// hsflow.hpp -- header-only C++ host layer over the C ABI (hsflow.h),
+// OpenCV-free.  Mirrors the reference's operator class
+// HornSchunckOF/hornSchunck.cpp:8-76 on plain image views:
+//
+//   hsflow::HornSchunck hs(windowSize, maxIterations, alpha);   // :13-17
+//   hs.getGradients(prev, next, gx, gy, gt);                      // :19-41
+//   hs.getFlow(prev, next, u, v);                                  // :43-75
+//
+// Same public fields, same argument meaning, outputs float64 row-major
+// (what CV_64FC1 holds).  Errors throw hsflow::Error (the reference throws
+// cv::Exception from inside OpenCV).  Copies share one device context, so a
+// copy-initialised object (main.cpp:97) reuses the cached device buffers.
+// Link: -lhsflow (cpp-optical-flow_amd/libhsflow.so).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hsflow.h"
+
+namespace hsflow {
+
+class Error : public std::runtime_error {
+  public:
+    Error(int status, const std::string &msg)
+        : std::runtime_error("hsflow: " + msg + " (" + hsflow_status_string(status) + ")"),
+          status_(status) {}
+    int status() const { return status_; }
+
+  private:
+    int status_;
+};
+
+// One single-channel image: U8 (CV_8UC1), F32 (CV_32FC1) or F64 (CV_64FC1);
+// `step` = bytes between rows (cv::Mat::step), so ROIs need no copy.
+struct ImageView {
+    const void *data = nullptr;
+    int rows = 0, cols = 0;
+    size_t step = 0;
+    int type = HSFLOW_U8;
+};
+
+inline ImageView view(const uint8_t *p, int rows, int cols, size_t step = 0) {
+    return {p, rows, cols, step ? step : (size_t)cols, HSFLOW_U8};
+}
+inline ImageView view(const float *p, int rows, int cols, size_t step = 0) {
+    return {p, rows, cols, step ? step : (size_t)cols * 4, HSFLOW_F32};
+}
+inline ImageView view(const double *p, int rows, int cols, size_t step = 0) {
+    return {p, rows, cols, step ? step : (size_t)cols * 8, HSFLOW_F64};
+}
+
+// RAII device context (device, stream, cached buffers).
+class Context {
+  public:
+    explicit Context(int device = 0) {
+        int rc = hsflow_create(&ctx_, device);
+        if (rc != HSFLOW_OK) throw Error(rc, hsflow_last_error(nullptr));
+    }
+    ~Context() { hsflow_destroy(ctx_); }
+    Context(const Context &) = delete;
+    Context &operator=(const Context &) = delete;
+    hsflow_ctx *get() const { return ctx_; }
+    void check(int rc) const {
+        if (rc != HSFLOW_OK) throw Error(rc, hsflow_last_error(ctx_));
+    }
+
+  private:
+    hsflow_ctx *ctx_ = nullptr;
+};
+
+class HornSchunck {
+  public:
+    // hornSchunck.cpp:10-11 -- public, same names
+    int windowSize, maxIterations;
+    double alpha;
+
+    // hornSchunck.cpp:13-17
+    HornSchunck(int inpWindowSize, int inpMaxIterations, double inpAlpha, int device = 0)
+        : windowSize(inpWindowSize), maxIterations(inpMaxIterations), alpha(inpAlpha),
+          device_(device) {}
+
+    // hornSchunck.cpp:19-41 -> Ix, Iy, It as rows*cols float64
+    void getGradients(const ImageView &imagePrev, const ImageView &imageNext,
+                      std::vector<double> &gradX, std::vector<double> &gradY,
+                      std::vector<double> &gradT) {
+        check_pair(imagePrev, imageNext);
+        const size_t n = (size_t)imagePrev.rows * imagePrev.cols;
+        gradX.resize(n);
+        gradY.resize(n);
+        gradT.resize(n);
+        Context &c = ctx();
+        c.check(hsflow_gradients(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
+                                 imagePrev.rows, imagePrev.cols, imagePrev.step,
+                                 gradX.data(), gradY.data(), gradT.data(), HSFLOW_F64,
+                                 (size_t)imagePrev.cols * 8));
+    }
+
+    // hornSchunck.cpp:43-75 -> u, v as rows*cols float64 (reallocated, like
+    // the reference's u = cv::Mat::zeros(...) at :49-50)
+    void getFlow(const ImageView &imagePrev, const ImageView &imageNext,
+                 std::vector<double> &u, std::vector<double> &v) {
+        check_pair(imagePrev, imageNext);
+        const size_t n = (size_t)imagePrev.rows * imagePrev.cols;
+        u.resize(n);
+        v.resize(n);
+        Context &c = ctx();
+        c.check(hsflow_flow(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
+                            imagePrev.rows, imagePrev.cols, imagePrev.step, windowSize,
+                            maxIterations, alpha, u.data(), v.data(), HSFLOW_F64,
+                            (size_t)imagePrev.cols * 8));
+    }
+
+    // Raw form for callers that own output rows (cv::Mat adapter): dtype_out
+    // HSFLOW_F64 or HSFLOW_F32, out_step in bytes.
+    void getFlowInto(const ImageView &imagePrev, const ImageView &imageNext, void *u,
+                     void *v, int dtype_out, size_t out_step) {
+        check_pair(imagePrev, imageNext);
+        Context &c = ctx();
+        c.check(hsflow_flow(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
+                            imagePrev.rows, imagePrev.cols, imagePrev.step, windowSize,
+                            maxIterations, alpha, u, v, dtype_out, out_step));
+    }
+    void getGradientsInto(const ImageView &imagePrev, const ImageView &imageNext, void *gx,
+                          void *gy, void *gt, int dtype_out, size_t out_step) {
+        check_pair(imagePrev, imageNext);
+        Context &c = ctx();
+        c.check(hsflow_gradients(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
+                                 imagePrev.rows, imagePrev.cols, imagePrev.step, gx, gy, gt,
+                                 dtype_out, out_step));
+    }
+
+  private:
+    int device_;
+    std::shared_ptr<Context> ctx_;
+
+    Context &ctx() {
+        if (!ctx_) ctx_ = std::make_shared<Context>(device_);
+        return *ctx_;
+    }
+    static void check_pair(const ImageView &a, const ImageView &b) {
+        if (!a.data || !b.data) throw Error(HSFLOW_ERR_ARG, "empty image");
+        if (a.rows != b.rows || a.cols != b.cols)
+            throw Error(HSFLOW_ERR_SIZE, "Image sizes are different");
+        if (a.type != b.type) throw Error(HSFLOW_ERR_ARG, "prev/next element types differ");
+    }
+};
+
+// compute(I0, I1, alpha, nIter) -> (u, v): the north-star convenience form.
+inline void compute(const ImageView &I0, const ImageView &I1, double alpha, int nIter,
+                    std::vector<double> &u, std::vector<double> &v, int windowSize = 5) {
+    HornSchunck(windowSize, nIter, alpha).getFlow(I0, I1, u, v);
+}
+
+}  // namespace hsflow
