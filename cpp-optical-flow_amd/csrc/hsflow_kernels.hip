@@ -341,11 +341,19 @@ template <int W, int KB>
 __global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
     constexpr int HL = KB * (W - W / 2 - 1);
     constexpr int OX = 64 - KB * (W - 1), OY = kRowsPacked - KB * (W - 1);
-    const int pair = blockIdx.y;
+    // XCD-aware block order.  Workgroups are dealt round-robin over the 8
+    // XCDs (linear id % 8 share an L2); remap so each XCD walks a contiguous
+    // run of tile rows and the halo rows/columns neighbouring regions re-read
+    // hit its L2.  Any bijection is correct; this one only changes speed.
+    const int nblk = gridDim.x * gridDim.y;
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nblk >> 3, rem = nblk & 7, xcd = lin & 7;
+    const int logical = xcd * q + min(xcd, rem) + (lin >> 3);
+    const int pair = logical / gridDim.x;
     const int lane = threadIdx.x & 63;
     // wave-uniform tile index (readfirstlane: keep tile maths in SGPRs)
-    const int tile =
-        blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int tile = (logical - pair * gridDim.x) * 4 +
+                     __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (tile >= p.tiles_x * p.tiles_y) return;
     const int ty = tile / p.tiles_x, tx = tile - ty * p.tiles_x;
     const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)p.cols;
