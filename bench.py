@@ -54,6 +54,11 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=0,
                     help="Jacobi iterations of the CPU sample (0: auto ~15 s)")
     ap.add_argument("--roofline-reps", type=int, default=3)
+    ap.add_argument("--mode", choices=["resident", "stream"], default="resident",
+                    help="resident: pairs generated on each rank, already in HBM "
+                         "(the metric); stream: BASELINE config 4, rank 0 holds "
+                         "--pairs pairs and scatters/gathers them over RCCL")
+    ap.add_argument("--pairs", type=int, default=64, help="stream mode: pairs in the stream")
     return ap.parse_args()
 
 
@@ -72,6 +77,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    if args.mode == "stream":
+        return stream_mode(args, world, rank, dev)
 
     wl = dict(WORKLOADS[args.workload])
     rows, cols = wl["rows"], wl["cols"]
@@ -182,6 +190,68 @@ def main():
             "sane": ok,
         }
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def stream_mode(args, world, rank, dev):
+    """BASELINE config 4: a stream of --pairs synthetic frame pairs held by
+    rank 0, scattered one-per-rank round-robin over RCCL (point-to-point),
+    solved (each rank batches its share into one hsflow_flow_device call),
+    and (u, v) gathered back to rank 0.  Timed end to end (scatter + solve +
+    gather), max over ranks.  Reported as pairs/s and Mpix*iter/s."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import hsflow
+    import frame_parallel as fp
+
+    wl = dict(WORKLOADS[args.workload])
+    rows, cols = wl["rows"], wl["cols"]
+    iters = args.iters or wl["iters"]
+    n = args.pairs
+    stream = None
+    if rank == 0:
+        stream = [tuple(torch.from_numpy(a).to(dev) for a in
+                        hsflow.synth_pair(1000 + j, rows, cols)) for j in range(n)]
+    mine = fp.my_pairs(n, rank, world)
+    ws = hsflow.alloc_workspace(rows, cols, max(1, len(mine)), dev)
+
+    def one_pass():
+        pairs = fp.scatter_pairs(stream, n, (rows, cols), torch.float32, dev, rank, world)
+        flows = []
+        if pairs:
+            I0 = torch.stack([p[0] for p in pairs])
+            I1 = torch.stack([p[1] for p in pairs])
+            u, v = hsflow.flow_device(I0, I1, args.window, iters, args.alpha, workspace=ws)
+            flows = [(u[k], v[k]) for k in range(len(pairs))]
+        return fp.gather_flows(flows, n, (rows, cols), dev, rank, world)
+
+    for _ in range(args.warmup):
+        one_pass()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one_pass()
+    torch.cuda.synchronize(dev)
+    elapsed = fp.max_over_ranks(time.perf_counter() - t0, dev, world)
+    if rank == 0:
+        ok = len(out) == n and all(bool(torch.isfinite(u).all()) for u, _ in out[:2])
+        total = n * args.steps
+        print(json.dumps({
+            "metric": "frame-pairs/s (config 4 stream: RCCL scatter + solve + gather)",
+            "value": round(total / elapsed, 2), "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic f32 frame pairs",
+            "config": {"workload": f"stream of {n} x {args.workload} pairs, {iters} it",
+                       "pairs": n, "iters": iters, "window": args.window,
+                       "parallelism": f"frame-parallel x{world}"},
+            "Mpix_iter_per_s": round(total * rows * cols * iters / elapsed / 1e6, 1),
+            "sane": ok}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,0 +1,114 @@
+"""Frame-parallel driver: a stream of frame pairs sharded across ranks.
+
+One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on
+MI355X, "gloo" for CPU tests).  Frame pairs are independent, so the only
+communication is moving data: rank 0 holds the stream, scatters pair j to
+rank j % world (point-to-point send/recv, batched; RCCL has no scatter
+primitive), every rank solves its pairs with libhsflow, and (u, v) are
+gathered back to rank 0 in stream order.  No reduction touches the hot path.
+
+The reference has no distributed code: this is the north_star's
+config 4 ("64 synthetic 1080p pairs sharded one-per-GPU, RCCL
+scatter/gather").  The per-pair solver is injected (`solve`), so the
+protocol is exercised with gloo + CPU tensors in tests while production uses
+hsflow.flow_device on the GPU.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+Pair = Tuple[torch.Tensor, torch.Tensor]
+
+
+def owner(j: int, world: int) -> int:
+    """Rank that solves pair j (round-robin, weak-scales with world)."""
+    return j % world
+
+
+def my_pairs(n_pairs: int, rank: int, world: int) -> List[int]:
+    return [j for j in range(n_pairs) if owner(j, world) == rank]
+
+
+def scatter_pairs(stream: Optional[Sequence[Pair]], n_pairs: int, shape, dtype, device,
+                  rank: int, world: int) -> List[Pair]:
+    """Rank 0 sends pair j to owner(j); returns this rank's pairs in order.
+    `stream` is only read on rank 0."""
+    mine = my_pairs(n_pairs, rank, world)
+    if world == 1:
+        return [(stream[j][0].to(device), stream[j][1].to(device)) for j in mine]
+    ops, out = [], []
+    if rank == 0:
+        for j in range(n_pairs):
+            dst = owner(j, world)
+            if dst == 0:
+                continue
+            I0, I1 = stream[j]
+            ops.append(dist.P2POp(dist.isend, I0.to(device).contiguous(), dst))
+            ops.append(dist.P2POp(dist.isend, I1.to(device).contiguous(), dst))
+        out = [(stream[j][0].to(device), stream[j][1].to(device)) for j in mine]
+    else:
+        for _ in mine:
+            a = torch.empty(shape, dtype=dtype, device=device)
+            b = torch.empty(shape, dtype=dtype, device=device)
+            ops.append(dist.P2POp(dist.irecv, a, 0))
+            ops.append(dist.P2POp(dist.irecv, b, 0))
+            out.append((a, b))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out
+
+
+def gather_flows(flows: List[Pair], n_pairs: int, shape, device, rank: int,
+                 world: int) -> Optional[List[Pair]]:
+    """Inverse of scatter_pairs for the (u, v) results; rank 0 returns the
+    full list in stream order, other ranks None."""
+    mine = my_pairs(n_pairs, rank, world)
+    if world == 1:
+        return list(flows)
+    ops = []
+    result: List[Optional[Pair]] = [None] * n_pairs
+    if rank == 0:
+        for k, j in enumerate(mine):
+            result[j] = flows[k]
+        for j in range(n_pairs):
+            src = owner(j, world)
+            if src == 0:
+                continue
+            u = torch.empty(shape, dtype=torch.float32, device=device)
+            v = torch.empty(shape, dtype=torch.float32, device=device)
+            ops.append(dist.P2POp(dist.irecv, u, src))
+            ops.append(dist.P2POp(dist.irecv, v, src))
+            result[j] = (u, v)
+    else:
+        for (u, v) in flows:
+            ops.append(dist.P2POp(dist.isend, u.contiguous(), 0))
+            ops.append(dist.P2POp(dist.isend, v.contiguous(), 0))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return result if rank == 0 else None
+
+
+def run_stream(stream: Optional[Sequence[Pair]], n_pairs: int, shape, dtype,
+               solve: Callable[[torch.Tensor, torch.Tensor], Pair], device,
+               rank: int, world: int, gather: bool = True):
+    """Scatter -> solve every owned pair -> gather.  Returns rank 0's list of
+    (u, v) in stream order (None elsewhere, or when gather=False)."""
+    pairs = scatter_pairs(stream, n_pairs, shape, dtype, device, rank, world)
+    flows = [solve(I0, I1) for (I0, I1) in pairs]
+    if not gather:
+        return None
+    return gather_flows(flows, n_pairs, shape, device, rank, world)
+
+
+def max_over_ranks(seconds: float, device, world: int) -> float:
+    """The bench's timing rule: the slowest rank defines the step time."""
+    if world == 1:
+        return seconds
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
