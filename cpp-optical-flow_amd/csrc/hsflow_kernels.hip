@@ -30,6 +30,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "hsflow_internal.h"
 
@@ -187,7 +188,7 @@ __device__ __forceinline__ float launder_f(float x) {
 template <int W, int KB, int RH, bool PACKED>
 __device__ __forceinline__ void jacobi_region(const JacobiArgs &p, size_t pbase,
                                               int plane_bytes, int lane, int gc, int r0,
-                                              int nout) {
+                                              int nout, int nout_cols = 64) {
     constexpr int A = W - W / 2 - 1;  // anchor (hornSchunck.cpp:54)
     constexpr int AR = W - 1 - A;     // taps right/below of the anchor
     constexpr int HL = KB * A, HR = KB * AR;
@@ -303,7 +304,7 @@ __device__ __forceinline__ void jacobi_region(const JacobiArgs &p, size_t pbase,
                                                              plane_bytes, 0x00020000);
         const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
                                                              plane_bytes, 0x00020000);
-        const bool st_lane = lane >= HL && lane < HL + OX && col_in;
+        const bool st_lane = lane >= HL && lane < HL + OX && (lane - HL) < nout_cols && col_in;
         const int off0 = launder(((r0 + HL) * cols + gc) * 4);
 #pragma unroll
         for (int r = HL; r < RH - HR; ++r) {
@@ -366,6 +367,251 @@ __global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
     }
     jacobi_region<W, KB, kRowsPacked, true>(p, pbase, plane_bytes, lane, gc, ty * OY - HL,
                                             OY);
+}
+
+// ------------------------------------------------------------------- K2 v2
+// Workgroup-stacked, two-columns-per-lane variant (windows 3 and 5, the
+// reference's 5 and the north-star's 3).
+//
+//  * A workgroup of NW waves covers a 128-column x NW*RW-row region; wave w
+//    owns slab rows [w*RW, (w+1)*RW), lane l owns columns 2l (e) and 2l+1 (o).
+//    Two columns per lane halve the horizontal halo share (KB(W-1) of 128
+//    instead of 64) and the cross-lane work per pixel.
+//  * The vertical window reaches A rows into the slab above and AR rows into
+//    the slab below.  Instead of recomputing those rows (temporal halo per
+//    wave), the stacked waves exchange their boundary rows through LDS once
+//    per iteration (double-buffered by iteration parity: one barrier per
+//    iteration).  Only the workgroup's outer rows carry a temporal halo.
+//  * Same per-pixel arithmetic as K2 except the horizontal sum association,
+//    which depends only on the column's parity within the region (region
+//    origins are even for every KB), so every KB gives identical bits.
+
+// Horizontal window sums of two columns per lane (e = even, o = odd column)
+// for two fields at once, statements interleaved for the DPP wait states.
+template <int W>
+__device__ __forceinline__ void hsum_c2(float ue, float uo, float ve, float vo, float &hue,
+                                        float &huo, float &hve, float &hvo) {
+    const float pu = ue + uo;
+    const float pv = ve + vo;
+    if constexpr (W == 5) {
+        // even 2l:   (x-2 + x-1) + (x + x+1) + x+2  = (P(l-1) + P(l)) + e(l+1)
+        // odd 2l+1:  (x-1 + (x + x+1)) + (x+2 + x+3) = (o(l-1) + P(l)) + P(l+1)
+        const float au = from_left(pu) + pu;
+        const float av = from_left(pv) + pv;
+        const float bu = from_left(uo) + pu;
+        const float bv = from_left(vo) + pv;
+        // launder pins each sum to its row: otherwise IR sinking moves the
+        // adds (and keeps the unfused DPP copies live) to the rows that use them
+        hue = launder_f(au + from_right(ue));
+        hve = launder_f(av + from_right(ve));
+        huo = launder_f(bu + from_right(pu));
+        hvo = launder_f(bv + from_right(pv));
+    } else {
+        static_assert(W == 3, "hsum_c2: windows 3 and 5");
+        // even 2l: x-1 + (x + x+1);  odd 2l+1: (x-1 + x) + x+1
+        hue = launder_f(from_left(uo) + pu);
+        hve = launder_f(from_left(vo) + pv);
+        huo = launder_f(pu + from_right(ue));
+        hvo = launder_f(pv + from_right(ve));
+    }
+}
+
+template <int W, int KB, int RW, int NW>
+__global__ __launch_bounds__(NW * 64) void hs_jacobi_wg_kernel(const JacobiArgs p) {
+    constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
+    constexpr int HL = KB * A, HR = KB * AR;  // temporal halo, rows
+    // column halo rounded up to even: region origins stay even for every KB,
+    // so a column's parity (which fixes its summation order) never changes
+    constexpr int HLc = HL + (HL & 1), HRc = HR + (HR & 1);
+    constexpr int RX = 128, RY = NW * RW;
+    constexpr int OX = RX - HLc - HRc, OY = RY - HL - HR;
+    constexpr int NB = A + AR;  // boundary rows a wave publishes per iteration
+    static_assert(OX > 0 && OY > 0 && (OX % 2) == 0, "geometry");
+    static_assert(RW <= 64, "row mask is 64 bits");
+    // [parity][wave][boundary row][field u/v][lane] of (even, odd) columns
+    __shared__ float2 xch[2][NW][NB][2][64];
+
+    // XCD-aware workgroup order (see hs_jacobi_kernel)
+    const int nblk = gridDim.x * gridDim.y;
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int qn = nblk >> 3, rem = nblk & 7, xcd = lin & 7;
+    const int logical = xcd * qn + min(xcd, rem) + (lin >> 3);
+    const int pair = logical / gridDim.x;
+    const int tile = logical - pair * gridDim.x;
+    if (tile >= p.tiles_x * p.tiles_y) return;  // whole workgroup: uniform
+    const int ty = tile / p.tiles_x, tx = tile - ty * p.tiles_x;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int cols = p.cols;
+    const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)cols;
+    const int plane_bytes = p.rows * cols * 4;
+
+    const uint32_t flag = p.flags != nullptr ? p.flags[pair] : 0u;
+    if (flag != 0u) {
+        // non-integral inputs: cover this workgroup's output tile with the
+        // f32-gradient regions of K2 (64 x 24, one wave each); no barriers
+        if constexpr (kb_ok_f32(W, KB)) {
+            constexpr int HLf = KB * A;
+            constexpr int OXf = 64 - KB * (W - 1), OYf = kRowsF32 - KB * (W - 1);
+            const int ox0 = tx * OX, oy0 = ty * OY;
+            constexpr int nsx = (OX + OXf - 1) / OXf, nsy = (OY + OYf - 1) / OYf;
+            for (int sidx = wv; sidx < nsx * nsy; sidx += NW) {
+                const int sy = sidx / nsx, sx = sidx - sy * nsx;
+                const int cx = ox0 + sx * OXf, cy = oy0 + sy * OYf;
+                jacobi_region<W, KB, kRowsF32, false>(p, pbase, plane_bytes, lane,
+                                                      cx - HLf + lane, cy - HLf,
+                                                      min(OYf, OY - sy * OYf),
+                                                      min(OXf, OX - sx * OXf));
+            }
+        }
+        return;
+    }
+
+    const int gce = tx * OX - HLc + 2 * lane;  // this lane's even image column
+    const int r0 = ty * OY - HL + wv * RW;    // image row of slab row 0
+    const bool ce = (unsigned)gce < (unsigned)cols;
+    const bool co = (unsigned)(gce + 1) < (unsigned)cols;
+    const int ce_i = ce ? 1 : 0, co_i = co ? 1 : 0;
+    uint64_t rowmask = 0;
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+        rowmask |= (uint64_t)((unsigned)(r0 + r) < (unsigned)p.rows) << r;
+
+    constexpr int kOOB = 0x7FFFFFF0;
+    const auto u_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase), 0, p.u_in ? plane_bytes : 0,
+        0x00020000);
+    const auto v_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(p.v_in ? p.v_in + pbase : p.v_out + pbase), 0, p.v_in ? plane_bytes : 0,
+        0x00020000);
+    const auto g_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gpack + pbase), 0,
+                                                        plane_bytes, 0x00020000);
+
+    float ue[RW], uo[RW], ve[RW], vo[RW];
+    uint32_t ge[RW], go[RW];
+    {
+        const int off0 = (r0 * cols + gce) * 4;
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const bool rin = (rowmask >> r) & 1ull;
+            const int oe = (rin && ce) ? off0 + r * cols * 4 : kOOB;
+            const int oo = (rin && co) ? off0 + r * cols * 4 + 4 : kOOB;
+            ue[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oe, 0, 0));
+            uo[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, 0));
+            ve[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, 0));
+            vo[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, 0));
+            ge[r] = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oe, 0, 0);
+            go[r] = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oo, 0, 0);
+        }
+    }
+
+    const float alpha2 = p.alpha2, inv = p.inv_w2;
+    auto update = [&](float su, float sv, uint32_t g, bool in, float &uu, float &vv) {
+        const float ub = su * inv, vb = sv * inv;
+        float ix, iy, itv;
+        unpack_grad(launder_u(g), ix, iy, itv);
+        // hornSchunck.cpp:63-73
+        const float den = alpha2 + ix * ix + iy * iy;
+        const float num = ix * ub + iy * vb + itv;
+        const float cc = num * __builtin_amdgcn_rcpf(den);
+        // laundered so the update stays in its row (IR sinking would move
+        // every row's update to the end of the iteration)
+        uu = launder_f(in ? ub - ix * cc : 0.f);
+        vv = launder_f(in ? vb - iy * cc : 0.f);
+    };
+
+    for (int it = 0; it < p.iters; ++it) {
+        const int par = it & 1;
+        // publish this slab's boundary rows (previous iteration's values):
+        // rows 0..AR-1 for the wave above, rows RW-A..RW-1 for the wave below
+#pragma unroll
+        for (int k = 0; k < AR; ++k) {
+            xch[par][wv][k][0][lane] = make_float2(ue[k], uo[k]);
+            xch[par][wv][k][1][lane] = make_float2(ve[k], vo[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < A; ++k) {
+            xch[par][wv][AR + k][0][lane] = make_float2(ue[RW - A + k], uo[RW - A + k]);
+            xch[par][wv][AR + k][1][lane] = make_float2(ve[RW - A + k], vo[RW - A + k]);
+        }
+        __syncthreads();
+
+        float hue[W], huo[W], hve[W], hvo[W], que[W], quo[W], qve[W], qvo[W];
+#pragma unroll
+        for (int rr = 0; rr < RW + NB; ++rr) {
+            const int r = rr - A;  // slab row, -A .. RW+AR-1
+            float xue, xuo, xve, xvo;
+            if (r < 0) {  // from the slab above (zero above the region)
+                float2 a = make_float2(0.f, 0.f), b = make_float2(0.f, 0.f);
+                if (wv > 0) {
+                    a = xch[par][wv - 1][AR + (r + A)][0][lane];
+                    b = xch[par][wv - 1][AR + (r + A)][1][lane];
+                }
+                xue = a.x; xuo = a.y; xve = b.x; xvo = b.y;
+            } else if (r >= RW) {  // from the slab below
+                float2 a = make_float2(0.f, 0.f), b = make_float2(0.f, 0.f);
+                if (wv < NW - 1) {
+                    a = xch[par][wv + 1][r - RW][0][lane];
+                    b = xch[par][wv + 1][r - RW][1][lane];
+                }
+                xue = a.x; xuo = a.y; xve = b.x; xvo = b.y;
+            } else {
+                xue = ue[r]; xuo = uo[r]; xve = ve[r]; xvo = vo[r];
+            }
+            const int sl = (r + 2 * W) % W;
+            hsum_c2<W>(xue, xuo, xve, xvo, hue[sl], huo[sl], hve[sl], hvo[sl]);
+            if (rr >= 1) {
+                const int sp = (r - 1 + 2 * W) % W;
+                que[sp] = hue[sp] + hue[sl];
+                quo[sp] = huo[sp] + huo[sl];
+                qve[sp] = hve[sp] + hve[sl];
+                qvo[sp] = hvo[sp] + hvo[sl];
+            }
+            const int y = r - AR;  // slab row whose window ends at r
+            if (y >= 0) {
+                float sue, suo, sve, svo;
+                if constexpr (W == 5) {
+                    // (h(y-2) + h(y-1)) + (h(y) + h(y+1)) + h(y+2)
+                    const int s0 = (y - 2 + 2 * W) % W, s1 = (y + 2 * W) % W,
+                              s2 = (y + 2 + 2 * W) % W;
+                    sue = (que[s0] + que[s1]) + hue[s2];
+                    suo = (quo[s0] + quo[s1]) + huo[s2];
+                    sve = (qve[s0] + qve[s1]) + hve[s2];
+                    svo = (qvo[s0] + qvo[s1]) + hvo[s2];
+                } else {
+                    // (h(y-1) + h(y)) + h(y+1)
+                    const int s0 = (y - 1 + 2 * W) % W, s2 = (y + 1 + 2 * W) % W;
+                    sue = que[s0] + hue[s2];
+                    suo = quo[s0] + huo[s2];
+                    sve = qve[s0] + hve[s2];
+                    svo = qvo[s0] + hvo[s2];
+                }
+                const bool rin = (rowmask >> y) & 1ull;  // no && : no branch
+                update(sue, sve, ge[y], rin & (launder(ce_i) != 0), ue[y], ve[y]);
+                update(suo, svo, go[y], rin & (launder(co_i) != 0), uo[y], vo[y]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // interior tile: workgroup rows [HL, HL + OY), lanes [HLc/2, (HLc + OX)/2)
+    const auto uo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_out + pbase), 0,
+                                                         plane_bytes, 0x00020000);
+    const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
+                                                         plane_bytes, 0x00020000);
+    const bool st_lane = lane >= HLc / 2 && lane < (HLc + OX) / 2;
+    const int off0 = launder((r0 * cols + gce) * 4);
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        const int wr = wv * RW + r;  // workgroup region row (wave-uniform)
+        const bool rin = wr >= HL && wr < HL + OY && ((rowmask >> r) & 1ull);
+        const int oe = (rin && st_lane && ce) ? off0 + r * cols * 4 : kOOB;
+        const int oo = (rin && st_lane && co) ? off0 + r * cols * 4 + 4 : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ue[r]), uo_rs, oe, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(uo[r]), uo_rs, oo, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ve[r]), vo_rs, oe, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo[r]), vo_rs, oo, 0, 0);
+    }
 }
 
 // ---------------------------------------------------------------------- K2g
@@ -453,8 +699,51 @@ bool kb_supported(int W, int KB, bool need_f32) {
     return need_f32 ? kb_ok_f32(W, KB) : kb_ok_packed(W, KB);
 }
 
+template <int W, int KB, int RW, int NW>
+static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
+    constexpr int HL = KB * (W - W / 2 - 1), HR = KB * (W / 2);
+    constexpr int OX = 128 - (HL + (HL & 1)) - (HR + (HR & 1));
+    constexpr int OY = NW * RW - KB * (W - 1);
+    a.tiles_x = (a.cols + OX - 1) / OX;
+    a.tiles_y = (a.rows + OY - 1) / OY;
+    const long ntiles = (long)a.tiles_x * a.tiles_y;
+    dim3 grd((unsigned)ntiles, (unsigned)a.batch, 1);
+    hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW>), grd, dim3(NW * 64), 0, s, a);
+    return hipGetLastError();
+}
+
+// K2 variant: 0 = per-wave regions (hs_jacobi_kernel), 16/20 = workgroup
+// kernel with 16/20-row slabs (windows 3 and 5).  HSFLOW_K2 env overrides.
+static int k2_variant() {
+    static int v = [] {
+        const char *e = getenv("HSFLOW_K2");
+        if (!e) return 16;
+        return atoi(e);
+    }();
+    return v;
+}
+
+template <int W, int KB>
+static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
+    switch (k2_variant()) {
+    case 20: return launch_jacobi_wg<W, KB, 20, 4>(a, s);
+    default: return launch_jacobi_wg<W, KB, 16, 4>(a, s);
+    }
+}
+
 template <int W>
 static hipError_t launch_jacobi_w(JacobiArgs a, int KB, hipStream_t s) {
+    if constexpr (W == 3 || W == 5) {
+        if (k2_variant() != 0) {
+            switch (KB) {
+            case 1: return launch_jacobi_wgv<W, 1>(a, s);
+            case 2: return launch_jacobi_wgv<W, 2>(a, s);
+            case 4: return launch_jacobi_wgv<W, 4>(a, s);
+            case 8: return launch_jacobi_wgv<W, 8>(a, s);
+            default: return hipErrorInvalidValue;
+            }
+        }
+    }
     switch (KB) {
     case 1: return launch_jacobi_t<W, 1>(a, s);
     case 2:
