@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -156,6 +157,11 @@ int jacobi_impl(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int 
     a.gy = w.gy;
     a.gt = w.gt;
     a.flags = w.flags;
+    static const int ablate = [] {
+        const char *e = getenv("HSFLOW_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    a.ablate = ablate;
     // pass p writes the caller's buffers iff (passes-1-p) is even, so the
     // last pass always lands in (u, v)
     auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };

@@ -173,6 +173,11 @@ __device__ __forceinline__ int launder(int x) {
     asm volatile("" : "+v"(x));
     return x;
 }
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v launder_v2(f2v x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 __device__ __forceinline__ uint32_t launder_u(uint32_t x) {
     asm volatile("" : "+v"(x));
     return x;
@@ -416,8 +421,15 @@ __device__ __forceinline__ void hsum_c2(float ue, float uo, float ve, float vo, 
     }
 }
 
-template <int W, int KB, int RW, int NW>
-__global__ __launch_bounds__(NW * 64) void hs_jacobi_wg_kernel(const JacobiArgs p) {
+template <int W, int KB, int RW, int NW, int SB, bool EDGE>
+__device__ __forceinline__ void wg_body(const JacobiArgs &p,
+                                        float2 (&xch)[2][NW][W - 1][2][64], int tx,
+                                        int ty, int wv, int lane, size_t pbase,
+                                        int plane_bytes);
+
+// 4 waves per SIMD (<= 128 VGPRs): two 8-wave workgroups per CU
+template <int W, int KB, int RW, int NW, int SB>
+__global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiArgs p) {
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
     constexpr int HL = KB * A, HR = KB * AR;  // temporal halo, rows
     // column halo rounded up to even: region origins stay even for every KB,
@@ -467,6 +479,28 @@ __global__ __launch_bounds__(NW * 64) void hs_jacobi_wg_kernel(const JacobiArgs 
         return;
     }
 
+    // interior workgroup: region + halo entirely inside the image, so no
+    // border masks (wave-uniform; the masked body handles the rest)
+    const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols &&
+                          ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows;
+    if (interior)
+        wg_body<W, KB, RW, NW, SB, false>(p, xch, tx, ty, wv, lane, pbase, plane_bytes);
+    else
+        wg_body<W, KB, RW, NW, SB, true>(p, xch, tx, ty, wv, lane, pbase, plane_bytes);
+}
+
+template <int W, int KB, int RW, int NW, int SB, bool EDGE>
+__device__ __forceinline__ void wg_body(const JacobiArgs &p,
+                                        float2 (&xch)[2][NW][W - 1][2][64], int tx,
+                                        int ty, int wv, int lane, size_t pbase,
+                                        int plane_bytes) {
+    constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
+    constexpr int HL = KB * A, HR = KB * AR;
+    constexpr int HLc = HL + (HL & 1), HRc = HR + (HR & 1);
+    constexpr int RX = 128;
+    constexpr int OX = RX - HLc - HRc, OY = NW * RW - HL - HR;
+    constexpr int NB = A + AR;
+    const int cols = p.cols;
     const int gce = tx * OX - HLc + 2 * lane;  // this lane's even image column
     const int r0 = ty * OY - HL + wv * RW;    // image row of slab row 0
     const bool ce = (unsigned)gce < (unsigned)cols;
@@ -478,17 +512,28 @@ __global__ __launch_bounds__(NW * 64) void hs_jacobi_wg_kernel(const JacobiArgs 
         rowmask |= (uint64_t)((unsigned)(r0 + r) < (unsigned)p.rows) << r;
 
     constexpr int kOOB = 0x7FFFFFF0;
+    const int nbytes = p.ablate == 2 ? 0 : plane_bytes;
     const auto u_rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase), 0, p.u_in ? plane_bytes : 0,
+        (void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase), 0, p.u_in ? nbytes : 0,
         0x00020000);
     const auto v_rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(p.v_in ? p.v_in + pbase : p.v_out + pbase), 0, p.v_in ? plane_bytes : 0,
+        (void *)(p.v_in ? p.v_in + pbase : p.v_out + pbase), 0, p.v_in ? nbytes : 0,
         0x00020000);
     const auto g_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gpack + pbase), 0,
-                                                        plane_bytes, 0x00020000);
+                                                        nbytes, 0x00020000);
 
-    float ue[RW], uo[RW], ve[RW], vo[RW];
-    uint32_t ge[RW], go[RW];
+    // (even, odd) column pairs as 2-wide vectors: the identical per-column
+    // arithmetic issues as packed FP32 (v_pk_add/mul/fma_f32), one
+    // instruction for both columns (on gfx950 a wave64 VALU op costs ~4 SIMD
+    // cycles and v_pk_*_f32 ~4.6 for twice the work: scripts/ubench).
+    //
+    // The per-pixel Jacobi operator is the same every iteration, so it is
+    // set up once per launch in normalised form:
+    //   s = 1/sqrt(alpha^2 + Ix^2 + Iy^2);  X = Ix s, Y = Iy s, T = It s
+    //   u' = ubar - X (X ubar + Y vbar + T),  v' = vbar - Y (...)
+    // which is hornSchunck.cpp:63-73 rearranged (c = (Ix ubar + Iy vbar +
+    // It)/D): 6 packed ops per column pair and no unpack / rcp per iteration.
+    f2v U[RW], V[RW], X[RW], Y[RW], T[RW];
     {
         const int off0 = (r0 * cols + gce) * 4;
 #pragma unroll
@@ -496,109 +541,133 @@ __global__ __launch_bounds__(NW * 64) void hs_jacobi_wg_kernel(const JacobiArgs 
             const bool rin = (rowmask >> r) & 1ull;
             const int oe = (rin && ce) ? off0 + r * cols * 4 : kOOB;
             const int oo = (rin && co) ? off0 + r * cols * 4 + 4 : kOOB;
-            ue[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oe, 0, 0));
-            uo[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, 0));
-            ve[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, 0));
-            vo[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, 0));
-            ge[r] = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oe, 0, 0);
-            go[r] = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oo, 0, 0);
+            U[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oe, 0, 0));
+            U[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, 0));
+            V[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, 0));
+            V[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, 0));
+            const uint32_t ge = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oe, 0, 0);
+            const uint32_t go = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oo, 0, 0);
+            float ixe, iye, ite, ixo, iyo, ito;
+            unpack_grad(ge, ixe, iye, ite);
+            unpack_grad(go, ixo, iyo, ito);
+            const float se = __builtin_amdgcn_rsqf(p.alpha2 + ixe * ixe + iye * iye);
+            const float so = __builtin_amdgcn_rsqf(p.alpha2 + ixo * ixo + iyo * iyo);
+            X[r] = f2v{ixe * se, ixo * so};
+            Y[r] = f2v{iye * se, iyo * so};
+            T[r] = f2v{ite * se, ito * so};
         }
     }
 
-    const float alpha2 = p.alpha2, inv = p.inv_w2;
-    auto update = [&](float su, float sv, uint32_t g, bool in, float &uu, float &vv) {
-        const float ub = su * inv, vb = sv * inv;
-        float ix, iy, itv;
-        unpack_grad(launder_u(g), ix, iy, itv);
-        // hornSchunck.cpp:63-73
-        const float den = alpha2 + ix * ix + iy * iy;
-        const float num = ix * ub + iy * vb + itv;
-        const float cc = num * __builtin_amdgcn_rcpf(den);
-        // laundered so the update stays in its row (IR sinking would move
-        // every row's update to the end of the iteration)
-        uu = launder_f(in ? ub - ix * cc : 0.f);
-        vv = launder_f(in ? vb - iy * cc : 0.f);
+    const float inv = p.inv_w2;
+    const f2v invv = {inv, inv};
+    // horizontal sums of slab row t (own data)
+    auto hrow = [&](int t, f2v &hu, f2v &hv) {
+        float a, b, c, d;
+        hsum_c2<W>(U[t].x, U[t].y, V[t].x, V[t].y, a, b, c, d);
+        hu = f2v{a, b};
+        hv = f2v{c, d};
     };
 
-    for (int it = 0; it < p.iters; ++it) {
+    const int n_it = p.ablate == 1 ? 0 : p.iters;
+    for (int it = 0; it < n_it; ++it) {
         const int par = it & 1;
-        // publish this slab's boundary rows (previous iteration's values):
-        // rows 0..AR-1 for the wave above, rows RW-A..RW-1 for the wave below
+        // 1. horizontal sums of the boundary rows first, published for the
+        //    neighbouring slabs: rows 0..AR-1 feed the wave above, rows
+        //    RW-A..RW-1 the wave below.  Exchanging sums (not raw rows)
+        //    means no wave recomputes another slab's rows.
+        f2v htu[AR], htv[AR], hbu[A], hbv[A];
 #pragma unroll
         for (int k = 0; k < AR; ++k) {
-            xch[par][wv][k][0][lane] = make_float2(ue[k], uo[k]);
-            xch[par][wv][k][1][lane] = make_float2(ve[k], vo[k]);
+            hrow(k, htu[k], htv[k]);
+            xch[par][wv][k][0][lane] = make_float2(htu[k].x, htu[k].y);
+            xch[par][wv][k][1][lane] = make_float2(htv[k].x, htv[k].y);
         }
 #pragma unroll
         for (int k = 0; k < A; ++k) {
-            xch[par][wv][AR + k][0][lane] = make_float2(ue[RW - A + k], uo[RW - A + k]);
-            xch[par][wv][AR + k][1][lane] = make_float2(ve[RW - A + k], vo[RW - A + k]);
+            hrow(RW - A + k, hbu[k], hbv[k]);
+            xch[par][wv][AR + k][0][lane] = make_float2(hbu[k].x, hbu[k].y);
+            xch[par][wv][AR + k][1][lane] = make_float2(hbv[k].x, hbv[k].y);
         }
         __syncthreads();
 
-        float hue[W], huo[W], hve[W], hvo[W], que[W], quo[W], qve[W], qvo[W];
+        // 2. sweep slab rows t = -A .. RW+AR-1 through a ring of horizontal
+        //    sums (hu, hv) and vertical pair sums q(t) = h(t) + h(t+1)
+        f2v hu[W], hv[W], qu[W], qv[W];
 #pragma unroll
         for (int rr = 0; rr < RW + NB; ++rr) {
-            const int r = rr - A;  // slab row, -A .. RW+AR-1
-            float xue, xuo, xve, xvo;
-            if (r < 0) {  // from the slab above (zero above the region)
+            const int t = rr - A;
+            const int sl = (t + 2 * W) % W;
+            if (t < 0) {  // the slab above's bottom rows (zero above the region)
                 float2 a = make_float2(0.f, 0.f), b = make_float2(0.f, 0.f);
                 if (wv > 0) {
-                    a = xch[par][wv - 1][AR + (r + A)][0][lane];
-                    b = xch[par][wv - 1][AR + (r + A)][1][lane];
+                    a = xch[par][wv - 1][AR + (t + A)][0][lane];
+                    b = xch[par][wv - 1][AR + (t + A)][1][lane];
                 }
-                xue = a.x; xuo = a.y; xve = b.x; xvo = b.y;
-            } else if (r >= RW) {  // from the slab below
+                hu[sl] = f2v{a.x, a.y};
+                hv[sl] = f2v{b.x, b.y};
+            } else if (t >= RW) {  // the slab below's top rows
                 float2 a = make_float2(0.f, 0.f), b = make_float2(0.f, 0.f);
                 if (wv < NW - 1) {
-                    a = xch[par][wv + 1][r - RW][0][lane];
-                    b = xch[par][wv + 1][r - RW][1][lane];
+                    a = xch[par][wv + 1][t - RW][0][lane];
+                    b = xch[par][wv + 1][t - RW][1][lane];
                 }
-                xue = a.x; xuo = a.y; xve = b.x; xvo = b.y;
+                hu[sl] = f2v{a.x, a.y};
+                hv[sl] = f2v{b.x, b.y};
+            } else if (t < AR) {
+                hu[sl] = htu[t];
+                hv[sl] = htv[t];
+            } else if (t >= RW - A) {
+                hu[sl] = hbu[t - (RW - A)];
+                hv[sl] = hbv[t - (RW - A)];
             } else {
-                xue = ue[r]; xuo = uo[r]; xve = ve[r]; xvo = vo[r];
+                hrow(t, hu[sl], hv[sl]);
             }
-            const int sl = (r + 2 * W) % W;
-            hsum_c2<W>(xue, xuo, xve, xvo, hue[sl], huo[sl], hve[sl], hvo[sl]);
             if (rr >= 1) {
-                const int sp = (r - 1 + 2 * W) % W;
-                que[sp] = hue[sp] + hue[sl];
-                quo[sp] = huo[sp] + huo[sl];
-                qve[sp] = hve[sp] + hve[sl];
-                qvo[sp] = hvo[sp] + hvo[sl];
+                const int sp = (t - 1 + 2 * W) % W;
+                qu[sp] = hu[sp] + hu[sl];
+                qv[sp] = hv[sp] + hv[sl];
             }
-            const int y = r - AR;  // slab row whose window ends at r
+            const int y = t - AR;  // slab row whose window ends at t
             if (y >= 0) {
-                float sue, suo, sve, svo;
+                f2v su, sv;
                 if constexpr (W == 5) {
                     // (h(y-2) + h(y-1)) + (h(y) + h(y+1)) + h(y+2)
                     const int s0 = (y - 2 + 2 * W) % W, s1 = (y + 2 * W) % W,
                               s2 = (y + 2 + 2 * W) % W;
-                    sue = (que[s0] + que[s1]) + hue[s2];
-                    suo = (quo[s0] + quo[s1]) + huo[s2];
-                    sve = (qve[s0] + qve[s1]) + hve[s2];
-                    svo = (qvo[s0] + qvo[s1]) + hvo[s2];
+                    su = (qu[s0] + qu[s1]) + hu[s2];
+                    sv = (qv[s0] + qv[s1]) + hv[s2];
                 } else {
                     // (h(y-1) + h(y)) + h(y+1)
                     const int s0 = (y - 1 + 2 * W) % W, s2 = (y + 1 + 2 * W) % W;
-                    sue = que[s0] + hue[s2];
-                    suo = quo[s0] + huo[s2];
-                    sve = qve[s0] + hve[s2];
-                    svo = qvo[s0] + hvo[s2];
+                    su = qu[s0] + hu[s2];
+                    sv = qv[s0] + hv[s2];
                 }
-                const bool rin = (rowmask >> y) & 1ull;  // no && : no branch
-                update(sue, sve, ge[y], rin & (launder(ce_i) != 0), ue[y], ve[y]);
-                update(suo, svo, go[y], rin & (launder(co_i) != 0), uo[y], vo[y]);
+                const f2v ub = su * invv, vb = sv * invv;
+                const f2v xv = X[y], yv = Y[y];
+                const f2v k = xv * ub + (yv * vb + T[y]);
+                f2v nu = ub - xv * k, nv = vb - yv * k;
+                if constexpr (EDGE) {
+                    // outside the image u = v = 0 (BORDER_CONSTANT)
+                    const bool rin = (rowmask >> y) & 1ull;
+                    const bool ie = rin & (launder(ce_i) != 0);
+                    const bool io = rin & (launder(co_i) != 0);
+                    nu.x = ie ? nu.x : 0.f;
+                    nu.y = io ? nu.y : 0.f;
+                    nv.x = ie ? nv.x : 0.f;
+                    nv.y = io ? nv.y : 0.f;
+                }
+                U[y] = nu;
+                V[y] = nv;
             }
-            __builtin_amdgcn_sched_barrier(0);
+            if ((rr % SB) == SB - 1) __builtin_amdgcn_sched_barrier(0);
         }
     }
 
     // interior tile: workgroup rows [HL, HL + OY), lanes [HLc/2, (HLc + OX)/2)
     const auto uo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_out + pbase), 0,
-                                                         plane_bytes, 0x00020000);
+                                                         nbytes, 0x00020000);
     const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
-                                                         plane_bytes, 0x00020000);
+                                                         nbytes, 0x00020000);
     const bool st_lane = lane >= HLc / 2 && lane < (HLc + OX) / 2;
     const int off0 = launder((r0 * cols + gce) * 4);
 #pragma unroll
@@ -607,10 +676,10 @@ __global__ __launch_bounds__(NW * 64) void hs_jacobi_wg_kernel(const JacobiArgs 
         const bool rin = wr >= HL && wr < HL + OY && ((rowmask >> r) & 1ull);
         const int oe = (rin && st_lane && ce) ? off0 + r * cols * 4 : kOOB;
         const int oo = (rin && st_lane && co) ? off0 + r * cols * 4 + 4 : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ue[r]), uo_rs, oe, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(uo[r]), uo_rs, oo, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ve[r]), vo_rs, oe, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo[r]), vo_rs, oo, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].x), uo_rs, oe, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].y), uo_rs, oo, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].x), vo_rs, oe, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, oo, 0, 0);
     }
 }
 
@@ -699,7 +768,7 @@ bool kb_supported(int W, int KB, bool need_f32) {
     return need_f32 ? kb_ok_f32(W, KB) : kb_ok_packed(W, KB);
 }
 
-template <int W, int KB, int RW, int NW>
+template <int W, int KB, int RW, int NW, int SB>
 static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     constexpr int HL = KB * (W - W / 2 - 1), HR = KB * (W / 2);
     constexpr int OX = 128 - (HL + (HL & 1)) - (HR + (HR & 1));
@@ -708,17 +777,17 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     a.tiles_y = (a.rows + OY - 1) / OY;
     const long ntiles = (long)a.tiles_x * a.tiles_y;
     dim3 grd((unsigned)ntiles, (unsigned)a.batch, 1);
-    hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW>), grd, dim3(NW * 64), 0, s, a);
+    hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW, SB>), grd, dim3(NW * 64), 0, s, a);
     return hipGetLastError();
 }
 
-// K2 variant: 0 = per-wave regions (hs_jacobi_kernel), 16/20 = workgroup
-// kernel with 16/20-row slabs (windows 3 and 5).  HSFLOW_K2 env overrides.
+// K2 variant (tuning; HSFLOW_K2 env): 0 = per-wave regions (hs_jacobi_kernel);
+// otherwise the workgroup kernel with slab rows RW and NW stacked waves:
+// 88 -> (8, 8) default, 816 -> (8, 16), 128 -> (12, 8), 164 -> (16, 4).
 static int k2_variant() {
     static int v = [] {
         const char *e = getenv("HSFLOW_K2");
-        if (!e) return 16;
-        return atoi(e);
+        return e ? atoi(e) : 88;
     }();
     return v;
 }
@@ -726,8 +795,10 @@ static int k2_variant() {
 template <int W, int KB>
 static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     switch (k2_variant()) {
-    case 20: return launch_jacobi_wg<W, KB, 20, 4>(a, s);
-    default: return launch_jacobi_wg<W, KB, 16, 4>(a, s);
+    case 816: return launch_jacobi_wg<W, KB, 8, 16, 1>(a, s);
+    case 128: return launch_jacobi_wg<W, KB, 12, 8, 1>(a, s);
+    case 164: return launch_jacobi_wg<W, KB, 16, 4, 1>(a, s);
+    default: return launch_jacobi_wg<W, KB, 8, 8, 1>(a, s);
     }
 }
 

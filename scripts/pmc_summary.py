@@ -17,7 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("prof"); ap.add_argument("tag")
 ap.add_argument("--workload", default="1080p"); ap.add_argument("--batch", type=int, default=8)
 ap.add_argument("--kb", type=int, default=4); ap.add_argument("--fetch-scale", type=float, default=1.0)
-ap.add_argument("--kernel", default="hs_jacobi_kernel")
+ap.add_argument("--kernel", default="hs_jacobi")
 a = ap.parse_args()
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 out = os.path.join(root, "profiles")
