@@ -131,6 +131,9 @@ def main():
     hsflow.gradients_device(I0, I1, ws, stream=stream)
     launches_per_solve = -(-iters // kb)
     reps = args.roofline_reps
+    # one stream here so the per-launch duration is what rocprofv3 reports
+    # per dispatch (the batch split overlaps launches and would blur it)
+    hsflow.set_max_streams(1)
     torch.cuda.synchronize(dev)
     ev0.record(stream)
     for _ in range(reps):
@@ -138,6 +141,7 @@ def main():
                              stream=stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
+    hsflow.set_max_streams(0)
     k2_ms = ev0.elapsed_time(ev1) / (reps * launches_per_solve)
     n_px = batch * px
     # compulsory bytes of one blocked pass: read u, v (f32) + packed gradients
@@ -182,7 +186,7 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "kernel": "hs_jacobi_kernel",
+                         "kernel": "hs_jacobi_wg_kernel",
                          "avg_launch_ms": round(k2_ms, 5),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "jacobi_equiv_GBps_28B": round(jacobi_equiv, 1)},

@@ -44,7 +44,7 @@ EXPORTS = (
     "hsflow_last_error", "hsflow_stream", "hsflow_flow", "hsflow_gradients",
     "hsflow_workspace_bytes", "hsflow_flow_device", "hsflow_gradients_device",
     "hsflow_jacobi_device", "hsflow_set_iters_per_launch", "hsflow_iters_per_launch",
-    "hsflow_bgr_to_gray", "hsflow_synth_pair",
+    "hsflow_bgr_to_gray", "hsflow_synth_pair", "hsflow_set_max_streams",
 )
 
 
@@ -100,6 +100,7 @@ def lib():
                                        _vp, _sz, _vp]
     L.hsflow_set_iters_per_launch.argtypes = [i]
     L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
+    L.hsflow_set_max_streams.argtypes = [i]
     L.hsflow_bgr_to_gray.argtypes = [_vp, i, i, _sz, _vp, _sz]
     L.hsflow_synth_pair.argtypes = [ctypes.c_uint64, i, i, i, i, _vp, _vp, _vp, _vp]
     _lib = L
@@ -320,6 +321,11 @@ def jacobi_device(rows, cols, batch, window, iters, alpha, u, v, workspace,
 
 def set_iters_per_launch(k: int):
     _check(lib().hsflow_set_iters_per_launch(int(k)))
+
+
+def set_max_streams(n: int):
+    """Side streams a batch is split over (1 = off, 0 = default)."""
+    _check(lib().hsflow_set_max_streams(int(n)))
 
 
 def iters_per_launch(rows, cols, batch, window) -> int:

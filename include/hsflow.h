@@ -118,6 +118,12 @@ int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
 int hsflow_set_iters_per_launch(int k);
 int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
 
+/* Batches of >= 2 pairs are split over up to n side streams (forked from and
+ * joined back to the caller's stream with events) so that concurrent Jacobi
+ * launches overlap their load and compute phases.  1 disables; 0 restores
+ * the default (8, or HSFLOW_STREAMS).  Process-wide. */
+int hsflow_set_max_streams(int n);
+
 /* ---- host utilities on the path to the hot loop ------------------------ */
 
 /* main.cpp:13-14 cv::cvtColor(BGR2GRAY) for 8-bit BGR, OpenCV 4.x 15-bit
