@@ -777,7 +777,14 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     a.tiles_y = (a.rows + OY - 1) / OY;
     const long ntiles = (long)a.tiles_x * a.tiles_y;
     dim3 grd((unsigned)ntiles, (unsigned)a.batch, 1);
-    hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW, SB>), grd, dim3(NW * 64), 0, s, a);
+    // diagnostics: HSFLOW_EXTRA_LDS bytes of unused dynamic LDS per workgroup
+    // (lowers the workgroups per CU; used to measure occupancy sensitivity)
+    static const unsigned extra_lds = [] {
+        const char *e = getenv("HSFLOW_EXTRA_LDS");
+        return e ? (unsigned)atoi(e) : 0u;
+    }();
+    hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW, SB>), grd, dim3(NW * 64),
+                       extra_lds, s, a);
     return hipGetLastError();
 }
 
