@@ -1,10 +1,12 @@
 """Horn-Schunck throughput bench (BASELINE.json metric: Mpix*iter/s + pairs/s).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1080p|4k]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1080p|4k|8k]
 
 One step = one full solve (K1 gradients + `iters` Jacobi iterations, the
 reference's getFlow, hornSchunck.cpp:43-75) of a batch of synthetic frame
-pairs per GPU, inputs already resident in HBM.  Frame pairs are independent,
+pairs per GPU, inputs already resident in HBM (workload 8k = BASELINE config
+5: an fp16 7680x4320 pair through the 3-level coarse-to-fine warm start,
+`iters` per level; its Mpix*iter counts every level's pixels).  Frame pairs are independent,
 so for N > 1 each rank (one process per GPU, torch.distributed over RCCL)
 solves its own pairs: weak scaling, no data-path collective (the timing
 barrier and max-over-ranks reduction are the only collectives).
@@ -33,6 +35,9 @@ WORKLOADS = {
     # BASELINE.json configs[1] / configs[2]
     "1080p": dict(rows=1080, cols=1920, iters=300, batch=8),
     "4k": dict(rows=2160, cols=3840, iters=500, batch=2),
+    # BASELINE.json configs[4] on one GPU (the 8-GPU row-band split is not a
+    # bench line; frame-parallel weak scaling is)
+    "8k": dict(rows=4320, cols=7680, iters=1000, batch=1, levels=3, dtype="f16"),
 }
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
@@ -47,8 +52,11 @@ def parse():
     ap.add_argument("--iters", type=int, default=0)
     ap.add_argument("--window", type=int, default=5)
     ap.add_argument("--alpha", type=float, default=1.0)
-    ap.add_argument("--dtype", choices=["f32", "u8"], default="f32",
-                    help="input frame element type (configs use f32)")
+    ap.add_argument("--dtype", choices=["f32", "u8", "f16"], default=None,
+                    help="input frame element type (default: the workload's, f32 "
+                         "for 1080p/4k, f16 for 8k)")
+    ap.add_argument("--levels", type=int, default=0,
+                    help="pyramid levels (default: the workload's; 1 = plain getFlow)")
     ap.add_argument("--kb", type=int, default=0, help="iterations per K2 launch (0 auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=0,
@@ -85,23 +93,33 @@ def main():
     rows, cols = wl["rows"], wl["cols"]
     iters = args.iters or wl["iters"]
     batch = args.batch or wl["batch"]
+    levels = args.levels or wl.get("levels", 1)
+    in_dtype = args.dtype or wl.get("dtype", "f32")
     if args.kb:
         hsflow.set_iters_per_launch(args.kb)
 
     # synthetic pairs, seed 1000 + global pair index
-    np_dtype = np.float32 if args.dtype == "f32" else np.uint8
+    np_dtype = np.uint8 if in_dtype == "u8" else np.float32
     pairs = [hsflow.synth_pair(1000 + rank * batch + i, rows, cols, dtype=np_dtype)
              for i in range(batch)]
     I0 = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
     I1 = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
     del pairs
+    if in_dtype == "f16":  # integer-valued 0..255: exact in fp16
+        I0, I1 = I0.half(), I1.half()
     u = torch.empty((batch, rows, cols), dtype=torch.float32, device=dev)
     v = torch.empty_like(u)
     ws = hsflow.alloc_workspace(rows, cols, batch, dev)
+    pws = (torch.empty(hsflow.pyramid_workspace_bytes(rows, cols, batch, levels),
+                       dtype=torch.uint8, device=dev) if levels > 1 else None)
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        hsflow.flow_device(I0, I1, args.window, iters, args.alpha, u, v, ws, stream)
+        if levels > 1:
+            hsflow.flow_pyramid_device(I0, I1, levels, args.window, iters, args.alpha, u, v,
+                                       pws, stream)
+        else:
+            hsflow.flow_device(I0, I1, args.window, iters, args.alpha, u, v, ws, stream)
 
     for _ in range(args.warmup):
         step()
@@ -121,8 +139,11 @@ def main():
         dist.barrier()
 
     px = rows * cols
+    # pixels swept per iteration, summed over the pyramid levels
+    px_all = sum(r * c for r, c in (hsflow.pyramid_level_size(rows, cols, l)
+                                    for l in range(levels)))
     total_pairs = batch * world * args.steps
-    value = total_pairs * px * iters / elapsed / 1e6
+    value = total_pairs * px_all * iters / elapsed / 1e6
     ok = bool(torch.isfinite(u).all().item()) and 0.05 < float(u.mean()) < 0.3
 
     # ---- dominant-kernel roofline: K2 alone, events on the launch stream --
@@ -176,9 +197,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic {args.dtype} frame pairs (hash texture, shift (-0.75,+1.5) px)",
-            "config": {"workload": f"{args.workload} {cols}x{rows}, {iters} it, ws {args.window}",
+            "data": f"synthetic {in_dtype} frame pairs (hash texture, shift (-0.75,+1.5) px)",
+            "config": {"workload": f"{args.workload} {cols}x{rows}, {iters} it"
+                                   + (f"/level x {levels} levels" if levels > 1 else "")
+                                   + f", ws {args.window}",
                        "rows": rows, "cols": cols, "iters": iters, "window": args.window,
+                       "levels": levels, "input_dtype": in_dtype,
                        "alpha": args.alpha, "pairs_per_gpu_per_step": batch,
                        "iters_per_launch": kb, "parallelism": f"frame-parallel x{world}"},
             "pairs_per_s": round(total_pairs / elapsed, 2),

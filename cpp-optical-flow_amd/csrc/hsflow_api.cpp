@@ -109,8 +109,16 @@ int elem_size(int dtype) {
     case HSFLOW_U8: return 1;
     case HSFLOW_F32: return 4;
     case HSFLOW_F64: return 8;
+    case HSFLOW_F16: return 2;
     default: return 0;
     }
+}
+
+// element size of the device copy of a host input (F64 is narrowed to f32)
+int dev_elem_size(int dtype) { return dtype == HSFLOW_F64 ? 4 : elem_size(dtype); }
+
+bool device_dtype_ok(int dtype) {
+    return dtype == HSFLOW_U8 || dtype == HSFLOW_F32 || dtype == HSFLOW_F16;
 }
 
 int pick_kb(int window, bool need_f32) {
@@ -320,8 +328,8 @@ int gradients_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in
                    void *workspace, size_t ws_bytes, hipStream_t s) {
     if (!sizes_ok(rows, cols, batch))
         return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
-    if (dtype_in != HSFLOW_U8 && dtype_in != HSFLOW_F32)
-        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8 or F32");
+    if (!device_dtype_ok(dtype_in))
+        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8, F16 or F32");
     if (!I0 || !I1 || !workspace) return fail(ctx, HSFLOW_ERR_ARG, "null device pointer");
     Workspace w = carve(workspace, rows, cols, batch);
     if (ws_bytes < w.bytes)
@@ -366,7 +374,7 @@ int grow_host(hsflow_ctx *ctx, size_t need) {
 // F64 input (CV_64FC1) is narrowed to f32 on the host first.
 int upload(hsflow_ctx *ctx, const void *src, int dtype, int rows, int cols, size_t step,
            void *dst, int *dev_dtype) {
-    if (dtype == HSFLOW_U8 || dtype == HSFLOW_F32) {
+    if (device_dtype_ok(dtype)) {
         const size_t es = (size_t)elem_size(dtype);
         HIP_TRY(ctx, hipMemcpy2DAsync(dst, cols * es, src, step, cols * es, rows,
                                       hipMemcpyHostToDevice, ctx->stream));
@@ -425,6 +433,99 @@ int check_host_args(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_i
         return fail(ctx, HSFLOW_ERR_ARG, "output dtype must be F32 or F64");
     if (out_step < (size_t)cols * elem_size(dtype_out))
         return fail(ctx, HSFLOW_ERR_ARG, "output step %zu < row bytes", out_step);
+    return HSFLOW_OK;
+}
+
+// ---- config 5 pyramid ----------------------------------------------------
+// Workspace: [Jacobi workspace of level 0][integrality flags][per level
+// l >= 1: I0_l, I1_l, u_l, v_l (batch x level plane, f32)].  Coarser levels
+// reuse the front of the level-0 Jacobi workspace.
+struct PyrLayout {
+    int levels;
+    int R[HSFLOW_MAX_LEVELS], C[HSFLOW_MAX_LEVELS];
+    size_t jac_bytes, flags_off;
+    size_t off[HSFLOW_MAX_LEVELS][4];  // I0, I1, u, v of level l >= 1
+    size_t bytes;
+};
+
+PyrLayout pyr_layout(int rows, int cols, int batch, int levels) {
+    PyrLayout L{};
+    L.levels = levels;
+    L.R[0] = rows;
+    L.C[0] = cols;
+    for (int l = 1; l < levels; ++l) {
+        L.R[l] = (L.R[l - 1] + 1) / 2;
+        L.C[l] = (L.C[l - 1] + 1) / 2;
+    }
+    L.jac_bytes = carve(nullptr, rows, cols, batch).bytes;
+    L.flags_off = L.jac_bytes;
+    size_t off = align_up(L.flags_off + (size_t)batch * 4);
+    for (int l = 1; l < levels; ++l) {
+        const size_t plane = align_up((size_t)L.R[l] * L.C[l] * batch * 4);
+        for (int k = 0; k < 4; ++k) {
+            L.off[l][k] = off;
+            off += plane;
+        }
+    }
+    L.bytes = off;
+    return L;
+}
+
+int pyramid_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, int rows,
+                 int cols, int batch, int levels, int window, int iters, float alpha,
+                 float *u, float *v, void *ws, size_t ws_bytes, hipStream_t s) {
+    if (levels < 1 || levels > HSFLOW_MAX_LEVELS)
+        return fail(ctx, HSFLOW_ERR_ARG, "levels %d outside [1, %d]", levels,
+                    HSFLOW_MAX_LEVELS);
+    if (!sizes_ok(rows, cols, batch))
+        return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
+    if (!device_dtype_ok(dtype_in))
+        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8, F16 or F32");
+    if (!I0 || !I1 || !u || !v || !ws)
+        return fail(ctx, HSFLOW_ERR_ARG, "null device pointer");
+    const PyrLayout L = pyr_layout(rows, cols, batch, levels);
+    if (ws_bytes < L.bytes)
+        return fail(ctx, HSFLOW_ERR_ARG, "workspace %zu < %zu bytes", ws_bytes, L.bytes);
+    const bool maybe_f32 = dtype_in != HSFLOW_U8;
+    char *base = (char *)ws;
+    int rc;
+    if (levels > 1) {
+        // integrality of each pair (K1's flag at level 0) decides the rounding
+        // of every level; saved because each level's K1 rewrites the flags
+        rc = gradients_impl(ctx, I0, I1, dtype_in, rows, cols, batch, nullptr, nullptr,
+                            nullptr, ws, L.jac_bytes, s);
+        if (rc) return rc;
+        uint32_t *intf = (uint32_t *)(base + L.flags_off);
+        HIP_TRY(ctx, hipMemcpyAsync(intf, carve(ws, rows, cols, batch).flags,
+                                    (size_t)batch * 4, hipMemcpyDeviceToDevice, s));
+        for (int l = 1; l < levels; ++l)
+            for (int k = 0; k < 2; ++k) {
+                const void *src = l == 1 ? (k ? I1 : I0) : base + L.off[l - 1][k];
+                hipError_t e = hsflow::launch_pyrdown(
+                    src, l == 1 ? dtype_in : HSFLOW_F32, L.R[l - 1], L.C[l - 1], batch,
+                    (float *)(base + L.off[l][k]), intf, s);
+                if (e != hipSuccess) return hip_fail(ctx, e, "pyrdown launch");
+            }
+    }
+    for (int l = levels - 1; l >= 0; --l) {
+        float *ul = l ? (float *)(base + L.off[l][2]) : u;
+        float *vl = l ? (float *)(base + L.off[l][3]) : v;
+        const bool warm = l < levels - 1;
+        if (warm) {
+            hipError_t e = hsflow::launch_upflow(
+                (const float *)(base + L.off[l + 1][2]), (const float *)(base + L.off[l + 1][3]),
+                L.R[l + 1], L.C[l + 1], ul, vl, L.R[l], L.C[l], batch, s);
+            if (e != hipSuccess) return hip_fail(ctx, e, "upflow launch");
+        }
+        rc = gradients_impl(ctx, l ? (const void *)(base + L.off[l][0]) : I0,
+                            l ? (const void *)(base + L.off[l][1]) : I1,
+                            l ? HSFLOW_F32 : dtype_in, L.R[l], L.C[l], batch, nullptr,
+                            nullptr, nullptr, ws, L.jac_bytes, s);
+        if (rc) return rc;
+        rc = jacobi_impl(ctx, L.R[l], L.C[l], batch, window, iters, alpha, warm, maybe_f32,
+                         ul, vl, ws, L.jac_bytes, s);
+        if (rc) return rc;
+    }
     return HSFLOW_OK;
 }
 
@@ -556,7 +657,7 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     if (iters < 0) return fail(ctx, HSFLOW_ERR_ARG, "maxIterations %d < 0", iters);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const size_t n = (size_t)rows * cols;
-    const size_t in_es = dtype_in == HSFLOW_U8 ? 1 : 4;
+    const size_t in_es = (size_t)dev_elem_size(dtype_in);
     if ((rc = grow(ctx, &ctx->d_in, &ctx->d_in_bytes, align_up(n * in_es) * 2))) return rc;
     if ((rc = grow(ctx, &ctx->d_out, &ctx->d_out_bytes, align_up(n * 4) * 3))) return rc;
     const size_t wsb = hsflow_workspace_bytes(rows, cols, 1);
@@ -577,6 +678,62 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     return HSFLOW_OK;
 }
 
+int hsflow_pyramid_level_size(int rows, int cols, int level, int *level_rows,
+                              int *level_cols) {
+    if (rows < 1 || cols < 1 || level < 0 || level >= HSFLOW_MAX_LEVELS) return HSFLOW_ERR_ARG;
+    for (int l = 0; l < level; ++l) {
+        rows = (rows + 1) / 2;
+        cols = (cols + 1) / 2;
+    }
+    if (level_rows) *level_rows = rows;
+    if (level_cols) *level_cols = cols;
+    return HSFLOW_OK;
+}
+
+size_t hsflow_pyramid_workspace_bytes(int rows, int cols, int batch, int levels) {
+    if (!sizes_ok(rows, cols, batch) || levels < 1 || levels > HSFLOW_MAX_LEVELS) return 0;
+    return pyr_layout(rows, cols, batch, levels).bytes;
+}
+
+int hsflow_flow_pyramid_device(const void *I0, const void *I1, int dtype_in, int rows,
+                               int cols, int batch, int levels, int window, int iters,
+                               float alpha, float *u, float *v, void *workspace,
+                               size_t workspace_bytes, void *stream) {
+    return pyramid_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, levels, window, iters,
+                        alpha, u, v, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
+                        int rows, int cols, size_t in_step, int levels, int window,
+                        int iters, double alpha, void *u, void *v, int dtype_out,
+                        size_t out_step) {
+    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step, dtype_out,
+                             out_step);
+    if (rc) return rc;
+    if (!u || !v) return fail(ctx, HSFLOW_ERR_ARG, "null output");
+    if (levels < 1 || levels > HSFLOW_MAX_LEVELS)
+        return fail(ctx, HSFLOW_ERR_ARG, "levels %d outside [1, %d]", levels,
+                    HSFLOW_MAX_LEVELS);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)rows * cols;
+    const size_t in_es = (size_t)dev_elem_size(dtype_in);
+    if ((rc = grow(ctx, &ctx->d_in, &ctx->d_in_bytes, align_up(n * in_es) * 2))) return rc;
+    if ((rc = grow(ctx, &ctx->d_out, &ctx->d_out_bytes, align_up(n * 4) * 3))) return rc;
+    const size_t wsb = hsflow_pyramid_workspace_bytes(rows, cols, 1, levels);
+    if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, wsb))) return rc;
+    char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
+    float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
+    int dt0 = 0, dt1 = 0;
+    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step, in0, &dt0))) return rc;
+    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step, in1, &dt1))) return rc;
+    rc = pyramid_impl(ctx, in0, in1, dt0, rows, cols, 1, levels, window, iters,
+                      (float)alpha, du, dv, ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
+    if (rc) return rc;
+    if ((rc = download(ctx, du, rows, cols, u, dtype_out, out_step))) return rc;
+    if ((rc = download(ctx, dv, rows, cols, v, dtype_out, out_step))) return rc;
+    return HSFLOW_OK;
+}
+
 int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
                      int rows, int cols, size_t in_step, void *gx, void *gy, void *gt,
                      int dtype_out, size_t out_step) {
@@ -586,7 +743,7 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
     if (!gx || !gy || !gt) return fail(ctx, HSFLOW_ERR_ARG, "null output");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const size_t n = (size_t)rows * cols;
-    const size_t in_es = dtype_in == HSFLOW_U8 ? 1 : 4;
+    const size_t in_es = (size_t)dev_elem_size(dtype_in);
     if ((rc = grow(ctx, &ctx->d_in, &ctx->d_in_bytes, align_up(n * in_es) * 2))) return rc;
     if ((rc = grow(ctx, &ctx->d_out, &ctx->d_out_bytes, align_up(n * 4) * 3))) return rc;
     const size_t wsb = hsflow_workspace_bytes(rows, cols, 1);

@@ -26,6 +26,11 @@ hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int ro
                             int cols, int batch, uint32_t *gpack, float *gx, float *gy,
                             float *gt, uint32_t *flags, hipStream_t s);
 hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s);
+// config 5 pyramid (hsflow_pyramid.hip); dtype as HSFLOW_U8/F32/F16
+hipError_t launch_pyrdown(const void *src, int dtype, int rows, int cols, int batch,
+                          float *dst, const uint32_t *flags, hipStream_t s);
+hipError_t launch_upflow(const float *uc, const float *vc, int rc, int cc, float *u,
+                         float *v, int rows, int cols, int batch, hipStream_t s);
 int default_kb(int W);
 bool kb_supported(int W, int KB, bool need_f32);
 

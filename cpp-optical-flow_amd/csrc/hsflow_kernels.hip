@@ -735,6 +735,10 @@ hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int ro
         hipLaunchKernelGGL(hs_gradients_kernel<uint8_t>, grd, blk, 0, s,
                            (const uint8_t *)I0, (const uint8_t *)I1, rows, cols, gpack,
                            gx, gy, gt, flags);
+    else if (dtype_in == 3)  // HSFLOW_F16 (config 5 inputs)
+        hipLaunchKernelGGL(hs_gradients_kernel<_Float16>, grd, blk, 0, s,
+                           (const _Float16 *)I0, (const _Float16 *)I1, rows, cols, gpack,
+                           gx, gy, gt, flags);
     else
         hipLaunchKernelGGL(hs_gradients_kernel<float>, grd, blk, 0, s,
                            (const float *)I0, (const float *)I1, rows, cols, gpack, gx,

@@ -6,8 +6,8 @@ Mirrors the reference's operator interface, HornSchunckOF/hornSchunck.cpp:
     gx, gy, gt = hs.getGradients(imagePrev, imageNext)       # :19-41
     u, v = hs.getFlow(imagePrev, imageNext)                  # :43-75
 
-with numpy arrays standing in for cv::Mat: inputs are 2-D uint8 / float32 /
-float64 (any row stride), outputs are float64 (CV_64FC1, what the reference
+with numpy arrays standing in for cv::Mat: inputs are 2-D uint8 / float16 /
+float32 / float64 (any row stride), outputs are float64 (CV_64FC1, what the reference
 returns and plotFlow.cpp:72-75 reads).  Also exposes the stream-ordered
 device entry points for torch tensors and the host utilities.
 
@@ -36,7 +36,8 @@ HSFLOW_ERR_HIP = -2
 HSFLOW_ERR_OOM = -3
 HSFLOW_ERR_NODEV = -4
 HSFLOW_ERR_SIZE = -5
-U8, F32, F64 = 0, 1, 2
+U8, F32, F64, F16 = 0, 1, 2, 3
+MAX_LEVELS = 8
 
 # every symbol include/hsflow.h declares
 EXPORTS = (
@@ -45,6 +46,8 @@ EXPORTS = (
     "hsflow_workspace_bytes", "hsflow_flow_device", "hsflow_gradients_device",
     "hsflow_jacobi_device", "hsflow_set_iters_per_launch", "hsflow_iters_per_launch",
     "hsflow_bgr_to_gray", "hsflow_synth_pair", "hsflow_set_max_streams",
+    "hsflow_pyramid_level_size", "hsflow_pyramid_workspace_bytes",
+    "hsflow_flow_pyramid_device", "hsflow_flow_pyramid",
 )
 
 
@@ -101,6 +104,13 @@ def lib():
     L.hsflow_set_iters_per_launch.argtypes = [i]
     L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
     L.hsflow_set_max_streams.argtypes = [i]
+    L.hsflow_pyramid_level_size.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.hsflow_pyramid_workspace_bytes.argtypes = [i, i, i, i]
+    L.hsflow_pyramid_workspace_bytes.restype = _sz
+    L.hsflow_flow_pyramid_device.argtypes = [_vp, _vp, i, i, i, i, i, i, i,
+                                             ctypes.c_float, _vp, _vp, _vp, _sz, _vp]
+    L.hsflow_flow_pyramid.argtypes = [_vp, _vp, _vp, i, i, i, _sz, i, i, i,
+                                      ctypes.c_double, _vp, _vp, i, _sz]
     L.hsflow_bgr_to_gray.argtypes = [_vp, i, i, _sz, _vp, _sz]
     L.hsflow_synth_pair.argtypes = [ctypes.c_uint64, i, i, i, i, _vp, _vp, _vp, _vp]
     _lib = L
@@ -121,6 +131,8 @@ def _dtype_code(a: np.ndarray) -> int:
         return F32
     if a.dtype == np.float64:
         return F64
+    if a.dtype == np.float16:
+        return F16
     raise HsflowError(HSFLOW_ERR_ARG, f"unsupported image dtype {a.dtype}")
 
 
@@ -175,6 +187,26 @@ class Context:
                                rows, cols, a.strides[0], int(window), int(iters),
                                float(alpha), u.ctypes.data, v.ctypes.data, code,
                                u.strides[0])
+        _check(rc, self._p)
+        return u, v
+
+    def flow_pyramid(self, I0, I1, levels: int, window: int, iters: int, alpha: float,
+                     out_dtype=np.float64):
+        """Config 5 coarse-to-fine warm start (`iters` per level), see
+        hsflow_flow_pyramid in include/hsflow.h."""
+        a, b = _as_image(I0), _as_image(I1)
+        if a.shape != b.shape:
+            raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
+        if a.dtype != b.dtype:
+            b = b.astype(a.dtype)
+        rows, cols = a.shape
+        u = np.empty((rows, cols), out_dtype)
+        v = np.empty((rows, cols), out_dtype)
+        code = F64 if u.dtype == np.float64 else F32
+        rc = lib().hsflow_flow_pyramid(self._p, a.ctypes.data, b.ctypes.data,
+                                       _dtype_code(a), rows, cols, a.strides[0],
+                                       int(levels), int(window), int(iters), float(alpha),
+                                       u.ctypes.data, v.ctypes.data, code, u.strides[0])
         _check(rc, self._p)
         return u, v
 
@@ -237,9 +269,12 @@ class hornSchunck:  # noqa: N801  (reference class name, hornSchunck.cpp:8)
         return uu, vv
 
 
-def compute(I0, I1, alpha: float, nIter: int, windowSize: int = 5):
+def compute(I0, I1, alpha: float, nIter: int, windowSize: int = 5, levels: int = 1):
     """compute(I0, I1, alpha, nIter) -> (u, v): the north-star convenience
-    wrapper over hornSchunck(windowSize, nIter, alpha).getFlow."""
+    wrapper over hornSchunck(windowSize, nIter, alpha).getFlow; levels > 1
+    runs the config-5 coarse-to-fine warm start (nIter per level)."""
+    if levels > 1:
+        return default_context().flow_pyramid(I0, I1, levels, windowSize, nIter, alpha)
     return hornSchunck(windowSize, nIter, alpha).getFlow(I0, I1)
 
 
@@ -264,7 +299,10 @@ def _tensor_dtype(t) -> int:
         return U8
     if t.dtype == torch.float32:
         return F32
-    raise HsflowError(HSFLOW_ERR_ARG, f"device input dtype {t.dtype} (want uint8/float32)")
+    if t.dtype == torch.float16:
+        return F16
+    raise HsflowError(HSFLOW_ERR_ARG,
+                      f"device input dtype {t.dtype} (want uint8/float16/float32)")
 
 
 def _check_dense(t, shape, name):
@@ -293,6 +331,43 @@ def flow_device(I0, I1, window: int, iters: int, alpha: float, u=None, v=None,
                                   cols, batch, int(window), int(iters), float(alpha),
                                   u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
                                   workspace.numel(), _stream_ptr(stream))
+    _check(rc)
+    return u, v
+
+
+def pyramid_level_size(rows: int, cols: int, level: int):
+    r, c = ctypes.c_int(), ctypes.c_int()
+    _check(lib().hsflow_pyramid_level_size(rows, cols, level, ctypes.byref(r),
+                                           ctypes.byref(c)))
+    return r.value, c.value
+
+
+def pyramid_workspace_bytes(rows: int, cols: int, batch: int, levels: int) -> int:
+    return int(lib().hsflow_pyramid_workspace_bytes(rows, cols, batch, levels))
+
+
+def flow_pyramid_device(I0, I1, levels: int, window: int, iters: int, alpha: float,
+                        u=None, v=None, workspace=None, stream=None):
+    """Config 5: coarse-to-fine warm start on torch CUDA tensors [B, H, W]
+    (uint8 / float16 / float32), `iters` Jacobi iterations per level."""
+    rows, cols = I0.shape[-2:]
+    batch = int(np.prod(I0.shape[:-2])) if I0.dim() > 2 else 1
+    _check_dense(I0, (rows, cols), "I0")
+    _check_dense(I1, (rows, cols), "I1")
+    if I1.dtype != I0.dtype or I1.shape != I0.shape:
+        raise HsflowError(HSFLOW_ERR_SIZE, "I0/I1 differ in shape or dtype")
+    if u is None:
+        u = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
+    if v is None:
+        v = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
+    if workspace is None:
+        n = pyramid_workspace_bytes(rows, cols, batch, levels)
+        workspace = torch.empty(n, dtype=torch.uint8, device=I0.device)
+    rc = lib().hsflow_flow_pyramid_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
+                                          rows, cols, batch, int(levels), int(window),
+                                          int(iters), float(alpha), u.data_ptr(),
+                                          v.data_ptr(), workspace.data_ptr(),
+                                          workspace.numel(), _stream_ptr(stream))
     _check(rc)
     return u, v
 

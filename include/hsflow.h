@@ -53,8 +53,9 @@ enum {
     HSFLOW_ERR_SIZE = -5   /* prev/next sizes differ (main.cpp:71-73)         */
 };
 
-/* Element types.  U8 = CV_8UC1, F32 = CV_32FC1, F64 = CV_64FC1. */
-enum { HSFLOW_U8 = 0, HSFLOW_F32 = 1, HSFLOW_F64 = 2 };
+/* Element types.  U8 = CV_8UC1, F32 = CV_32FC1, F64 = CV_64FC1,
+ * F16 = CV_16FC1 (config 5 inputs; input only). */
+enum { HSFLOW_U8 = 0, HSFLOW_F32 = 1, HSFLOW_F64 = 2, HSFLOW_F16 = 3 };
 
 /* Largest windowSize accepted (hornSchunck.cpp:53 allows any; OpenCV would
  * take a few seconds per iteration at this size already). */
@@ -90,7 +91,7 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
 /* ---- device pointers, stream-ordered ------------------------------------
  * A batch is `batch` independent frame pairs stored back to back:
  * I0[b][rows][cols], dense (pitch = cols elements), likewise u, v.
- * Inputs are U8 or F32.  Outputs are f32.  `stream` is a hipStream_t (NULL =
+ * Inputs are U8, F16 or F32.  Outputs are f32.  `stream` is a hipStream_t (NULL =
  * default stream).  `workspace` is device memory of at least
  * hsflow_workspace_bytes(rows, cols, batch) bytes, 256-byte aligned. */
 size_t hsflow_workspace_bytes(int rows, int cols, int batch);
@@ -123,6 +124,33 @@ int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
  * launches overlap their load and compute phases.  1 disables; 0 restores
  * the default (8, or HSFLOW_STREAMS).  Process-wide. */
 int hsflow_set_max_streams(int n);
+
+/* ---- coarse-to-fine warm start (north_star config 5) ---------------------
+ * The reference's HS has no pyramid; the repository's own multi-resolution
+ * code is the precedent (BMOpticalFlow/.../OpticalFlow/MultiResolution.cpp:
+ * 9-97 Pyramider, OpticalFlow.cpp:197-210 Add_VectorOffset).  Level l is
+ * ceil(rows / 2^l) x ceil(cols / 2^l), made from level l-1 by the 5-tap
+ * kernel (2,5,4,5,2)/18 per axis (a = 0.4), stride 2, reflect-101; levels of
+ * integer-valued pairs are rounded half-up to integers.  The coarsest level
+ * starts from u = v = 0, every finer one from u = 2 u_coarse(y/2, x/2)
+ * (likewise v); each level runs `iters` Jacobi iterations of the getFlow
+ * loop (hornSchunck.cpp:56-74) on its own gradients.  levels = 1 is
+ * hsflow_flow_device exactly. */
+#define HSFLOW_MAX_LEVELS 8
+
+/* Size of pyramid level `level` (0 = full size). */
+int hsflow_pyramid_level_size(int rows, int cols, int level, int *level_rows,
+                              int *level_cols);
+size_t hsflow_pyramid_workspace_bytes(int rows, int cols, int batch, int levels);
+int hsflow_flow_pyramid_device(const void *I0, const void *I1, int dtype_in, int rows,
+                               int cols, int batch, int levels, int window, int iters,
+                               float alpha, float *u, float *v, void *workspace,
+                               size_t workspace_bytes, void *stream);
+/* Host-buffer, blocking form (same conventions as hsflow_flow). */
+int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
+                        int rows, int cols, size_t in_step, int levels, int window,
+                        int iters, double alpha, void *u, void *v, int dtype_out,
+                        size_t out_step);
 
 /* ---- host utilities on the path to the hot loop ------------------------ */
 

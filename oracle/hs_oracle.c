@@ -163,6 +163,82 @@ void hso_flow(const double *I0, const double *I1, int rows, int cols, int window
     free(gx); free(gy); free(gt);
 }
 
+/* ---- config 5 pyramid (see hs_oracle.h) ------------------------------- */
+static const double kPyrW[5] = {2.0, 5.0, 4.0, 5.0, 2.0}; /* a = 0.4, x 9 / 0.5 */
+
+void hso_pyrdown(const double *src, int rows, int cols, int round_int, double *dst) {
+    const int r2 = (rows + 1) / 2, c2 = (cols + 1) / 2;
+    for (int y = 0; y < r2; ++y)
+        for (int x = 0; x < c2; ++x) {
+            /* MultiResolution.cpp:80-87: ym = 2y + m - 2, xn = 2x + n - 2 */
+            double S = 0.0;
+            for (int m = 0; m < 5; ++m) {
+                const double *row = src + (size_t)reflect101(2 * y + m - 2, rows) * cols;
+                double h = 0.0;
+                for (int n = 0; n < 5; ++n) h += kPyrW[n] * row[reflect101(2 * x + n - 2, cols)];
+                S += kPyrW[m] * h;
+            }
+            dst[(size_t)y * c2 + x] = round_int ? floor((S + 162.0) / 324.0) : S / 324.0;
+        }
+}
+
+int hso_integer_pair(const double *I0, const double *I1, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        const double a = I0[i], b = I1[i];
+        if (a != floor(a) || b != floor(b) || a < 0 || a > 255 || b < 0 || b > 255)
+            return 0;
+    }
+    return 1;
+}
+
+void hso_flow_pyramid(const double *I0, const double *I1, int rows, int cols,
+                      int levels, int window, int iters, double alpha, double *u,
+                      double *v, int nthreads) {
+    if (levels < 1) levels = 1;
+    if (levels > 16) levels = 16;
+    const int rnd = hso_integer_pair(I0, I1, (size_t)rows * cols);
+    int R[16], C[16];
+    double *P0[16], *P1[16], *U[16], *V[16];
+    R[0] = rows; C[0] = cols;
+    P0[0] = (double *)I0; P1[0] = (double *)I1;
+    for (int l = 1; l < levels; ++l) {
+        R[l] = (R[l - 1] + 1) / 2;
+        C[l] = (C[l - 1] + 1) / 2;
+        P0[l] = (double *)malloc((size_t)R[l] * C[l] * sizeof(double));
+        P1[l] = (double *)malloc((size_t)R[l] * C[l] * sizeof(double));
+        hso_pyrdown(P0[l - 1], R[l - 1], C[l - 1], rnd, P0[l]);
+        hso_pyrdown(P1[l - 1], R[l - 1], C[l - 1], rnd, P1[l]);
+    }
+    for (int l = levels - 1; l >= 0; --l) {
+        const size_t n = (size_t)R[l] * C[l];
+        U[l] = l ? (double *)malloc(n * sizeof(double)) : u;
+        V[l] = l ? (double *)malloc(n * sizeof(double)) : v;
+        if (l == levels - 1) {
+            memset(U[l], 0, n * sizeof(double));
+            memset(V[l], 0, n * sizeof(double));
+        } else { /* OpticalFlow.cpp:205-206 */
+            for (int y = 0; y < R[l]; ++y)
+                for (int x = 0; x < C[l]; ++x) {
+                    const size_t c = (size_t)(y / 2) * C[l + 1] + x / 2;
+                    U[l][(size_t)y * C[l] + x] = 2.0 * U[l + 1][c];
+                    V[l][(size_t)y * C[l] + x] = 2.0 * V[l + 1][c];
+                }
+            free(U[l + 1]);
+            free(V[l + 1]);
+        }
+        double *gx = (double *)malloc(n * sizeof(double));
+        double *gy = (double *)malloc(n * sizeof(double));
+        double *gt = (double *)malloc(n * sizeof(double));
+        hso_gradients(P0[l], P1[l], R[l], C[l], gx, gy, gt);
+        hso_jacobi(gx, gy, gt, R[l], C[l], window, iters, alpha, U[l], V[l], nthreads);
+        free(gx); free(gy); free(gt);
+    }
+    for (int l = 1; l < levels; ++l) {
+        free(P0[l]);
+        free(P1[l]);
+    }
+}
+
 /* ---- plotFlow.cpp, headless ------------------------------------------- */
 
 static int sgn(int x) { return x < 0 ? -1 : (x > 0 ? 1 : 0); } /* :24-28 */

@@ -52,6 +52,32 @@ void hso_jacobi(const double *gx, const double *gy, const double *gt,
                 int rows, int cols, int window, int iters, double alpha,
                 double *u, double *v, int nthreads);
 
+/* ---- config 5: coarse-to-fine pyramid warm start ----
+ * HornSchunckOF has no pyramid; the design precedent is the repository's
+ * BM module: Pyramider (BMOpticalFlow/.../OpticalFlow/MultiResolution.cpp:
+ * 9-97: 5-tap kernel w = (a/2, 1/2, a, 1/2, a/2)/sum, a = 0.4, i.e.
+ * (2,5,4,5,2)/18, stride 2, level size ceil(n / 2^l), mirrored border) and
+ * Add_VectorOffset (OpticalFlow.cpp:197-210: u_l(x,y) += 2 u_{l+1}(x/2,y/2)).
+ * The mirror border (ImgVector::get_mirror, not vendored) is taken as
+ * reflect-101.  Levels of an integer-valued pair (every pixel of both
+ * frames an integer in [0, 255]) are rounded half-up to integers, as an
+ * 8-bit pyrDown would:  L = floor((S + 162) / 324), S = sum w_m w_n I;
+ * other pairs keep S / 324. */
+
+/* One level down: src rows x cols -> dst ceil(rows/2) x ceil(cols/2). */
+void hso_pyrdown(const double *src, int rows, int cols, int round_int, double *dst);
+
+/* 1 if every pixel of both frames is an integer in [0, 255]. */
+int hso_integer_pair(const double *I0, const double *I1, size_t n);
+
+/* Coarse to fine over `levels` levels (1 = hso_flow): at the coarsest level
+ * u = v = 0; each finer level starts from u = 2 u_coarse(y/2, x/2) (same for
+ * v) and runs `iters` Jacobi iterations of hornSchunck.cpp:56-74 on its own
+ * gradients.  u, v: rows x cols (level 0). */
+void hso_flow_pyramid(const double *I0, const double *I1, int rows, int cols,
+                      int levels, int window, int iters, double alpha, double *u,
+                      double *v, int nthreads);
+
 /* plotFlow.cpp:68-88 without namedWindow/imshow.  Draws into `bgr`
  * (rows x cols x 3, dense) in place. */
 void hso_plot_bresenham(uint8_t *bgr, int rows, int cols, const double *u,

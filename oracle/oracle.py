@@ -37,6 +37,11 @@ def lib():
                                ctypes.c_int, ctypes.c_double, _dp, _dp, ctypes.c_int]
         L.hso_jacobi.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_double, _dp, _dp, ctypes.c_int]
+        L.hso_pyrdown.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]
+        L.hso_integer_pair.argtypes = [_dp, _dp, ctypes.c_size_t]
+        L.hso_flow_pyramid.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_double, _dp,
+                                       _dp, ctypes.c_int]
         L.hso_plot_bresenham.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, _dp, _dp,
                                          ctypes.c_int, ctypes.c_float, ctypes.c_int]
         _lib = L
@@ -88,6 +93,31 @@ def jacobi(gx, gy, gt, u0, v0, window: int, iters: int, alpha: float, nthreads: 
     rows, cols = gx.shape
     lib().hso_jacobi(_d(gx), _d(gy), _d(gt), rows, cols, int(window), int(iters),
                      float(alpha), _d(u), _d(v), int(nthreads))
+    return u, v
+
+
+def integer_pair(I0, I1) -> bool:
+    a, b = _f64(I0), _f64(I1)
+    return bool(lib().hso_integer_pair(_d(a), _d(b), a.size))
+
+
+def pyrdown(img, round_int: bool):
+    """One pyramid level down (MultiResolution.cpp:9-97 kernel, see hs_oracle.h)."""
+    a = _f64(img)
+    rows, cols = a.shape
+    out = np.empty(((rows + 1) // 2, (cols + 1) // 2), np.float64)
+    lib().hso_pyrdown(_d(a), rows, cols, int(bool(round_int)), _d(out))
+    return out
+
+
+def flow_pyramid(I0, I1, levels: int, window: int, iters: int, alpha: float,
+                 nthreads: int = 1):
+    """Config 5: coarse-to-fine warm start, `iters` per level -> (u, v) f64."""
+    a, b = _f64(I0), _f64(I1)
+    rows, cols = a.shape
+    u, v = np.empty_like(a), np.empty_like(a)
+    lib().hso_flow_pyramid(_d(a), _d(b), rows, cols, int(levels), int(window),
+                           int(iters), float(alpha), _d(u), _d(v), int(nthreads))
     return u, v
 
 
