@@ -734,6 +734,60 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
     return HSFLOW_OK;
 }
 
+int hsflow_bgr_to_gray_device(const uint8_t *bgr, int rows, int cols, int batch,
+                              uint8_t *gray, void *stream) {
+    if (!bgr || !gray) return fail(nullptr, HSFLOW_ERR_ARG, "null device pointer");
+    if (!sizes_ok(rows, cols, batch))
+        return fail(nullptr, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
+    hipError_t e = hsflow::launch_bgr2gray(bgr, rows, cols, batch, gray, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(nullptr, e, "bgr2gray launch");
+    return HSFLOW_OK;
+}
+
+int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, int rows,
+                    int cols, size_t bgr_step, int window, int iters, double alpha,
+                    void *u, void *v, int dtype_out, size_t out_step) {
+    if (!ctx) return HSFLOW_ERR_ARG;
+    if (!bgr0 || !bgr1 || !u || !v) return fail(ctx, HSFLOW_ERR_ARG, "null pointer");
+    if (!sizes_ok(rows, cols, 1)) return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d", rows, cols);
+    if (bgr_step < (size_t)cols * 3)
+        return fail(ctx, HSFLOW_ERR_ARG, "BGR step %zu < row bytes", bgr_step);
+    if (dtype_out != HSFLOW_F32 && dtype_out != HSFLOW_F64)
+        return fail(ctx, HSFLOW_ERR_ARG, "output dtype must be F32 or F64");
+    if (out_step < (size_t)cols * elem_size(dtype_out))
+        return fail(ctx, HSFLOW_ERR_ARG, "output step %zu < row bytes", out_step);
+    if (window < 1 || window > HSFLOW_MAX_WINDOW)
+        return fail(ctx, HSFLOW_ERR_ARG, "windowSize %d outside [1, %d]", window,
+                    HSFLOW_MAX_WINDOW);
+    if (iters < 0) return fail(ctx, HSFLOW_ERR_ARG, "maxIterations %d < 0", iters);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)rows * cols;
+    // [bgr0 bgr1] back to back (one batch-2 launch), then [gray0 gray1]
+    const size_t gray_off = align_up(6 * n);
+    int rc;
+    if ((rc = grow(ctx, &ctx->d_in, &ctx->d_in_bytes, gray_off + align_up(2 * n)))) return rc;
+    if ((rc = grow(ctx, &ctx->d_out, &ctx->d_out_bytes, align_up(n * 4) * 3))) return rc;
+    if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, hsflow_workspace_bytes(rows, cols, 1))))
+        return rc;
+    uint8_t *db = (uint8_t *)ctx->d_in, *dg = db + gray_off;
+    HIP_TRY(ctx, hipMemcpy2DAsync(db, (size_t)cols * 3, bgr0, bgr_step, (size_t)cols * 3, rows,
+                                  hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(db + 3 * n, (size_t)cols * 3, bgr1, bgr_step,
+                                  (size_t)cols * 3, rows, hipMemcpyHostToDevice, ctx->stream));
+    hipError_t e = hsflow::launch_bgr2gray(db, rows, cols, 2, dg, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "bgr2gray launch");
+    float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
+    rc = gradients_impl(ctx, dg, dg + n, HSFLOW_U8, rows, cols, 1, nullptr, nullptr, nullptr,
+                        ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
+    if (rc) return rc;
+    rc = jacobi_impl(ctx, rows, cols, 1, window, iters, (float)alpha, false, false, du, dv,
+                     ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
+    if (rc) return rc;
+    if ((rc = download(ctx, du, rows, cols, u, dtype_out, out_step))) return rc;
+    if ((rc = download(ctx, dv, rows, cols, v, dtype_out, out_step))) return rc;
+    return HSFLOW_OK;
+}
+
 int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
                      int rows, int cols, size_t in_step, void *gx, void *gy, void *gt,
                      int dtype_out, size_t out_step) {

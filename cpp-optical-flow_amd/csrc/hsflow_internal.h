@@ -29,6 +29,9 @@ hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s);
 // config 5 pyramid (hsflow_pyramid.hip); dtype as HSFLOW_U8/F32/F16
 hipError_t launch_pyrdown(const void *src, int dtype, int rows, int cols, int batch,
                           float *dst, const uint32_t *flags, hipStream_t s);
+// GPU input path (hsflow_input.hip): dense BGR u8 planes -> gray u8
+hipError_t launch_bgr2gray(const uint8_t *bgr, int rows, int cols, int batch,
+                           uint8_t *gray, hipStream_t s);
 hipError_t launch_upflow(const float *uc, const float *vc, int rc, int cc, float *u,
                          float *v, int rows, int cols, int batch, hipStream_t s);
 int default_kb(int W);

@@ -174,6 +174,7 @@ __device__ __forceinline__ int launder(int x) {
     return x;
 }
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v launder_v2(f2v x) {
     asm volatile("" : "+v"(x));
     return x;
@@ -481,8 +482,11 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
 
     // interior workgroup: region + halo entirely inside the image, so no
     // border masks (wave-uniform; the masked body handles the rest)
+    // interior: the whole region lies inside the image, and rows are 8-byte
+    // aligned (even width) so the column pairs move as single 8-byte words
     const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols &&
-                          ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows;
+                          ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows &&
+                          (cols & 1) == 0;
     if (interior)
         wg_body<W, KB, RW, NW, SB, false>(p, xch, tx, ty, wv, lane, pbase, plane_bytes);
     else
@@ -538,15 +542,30 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
         const int off0 = (r0 * cols + gce) * 4;
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-            const bool rin = (rowmask >> r) & 1ull;
-            const int oe = (rin && ce) ? off0 + r * cols * 4 : kOOB;
-            const int oo = (rin && co) ? off0 + r * cols * 4 + 4 : kOOB;
-            U[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oe, 0, 0));
-            U[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, 0));
-            V[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, 0));
-            V[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, 0));
-            const uint32_t ge = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oe, 0, 0);
-            const uint32_t go = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oo, 0, 0);
+            uint32_t ge, go;
+            if constexpr (!EDGE) {
+                // interior tile of an even-width image: the lane's column
+                // pair is one aligned 8-byte word -> fully coalesced 512 B
+                // per wave instruction (vs two half-line stride-2 loads)
+                const int o = off0 + r * cols * 4;
+                const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, 0);
+                const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, 0);
+                const u2v g = __builtin_amdgcn_raw_buffer_load_b64(g_rs, o, 0, 0);
+                U[r] = f2v{__uint_as_float(a.x), __uint_as_float(a.y)};
+                V[r] = f2v{__uint_as_float(b.x), __uint_as_float(b.y)};
+                ge = g.x;
+                go = g.y;
+            } else {
+                const bool rin = (rowmask >> r) & 1ull;
+                const int oe = (rin && ce) ? off0 + r * cols * 4 : kOOB;
+                const int oo = (rin && co) ? off0 + r * cols * 4 + 4 : kOOB;
+                U[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oe, 0, 0));
+                U[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, 0));
+                V[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, 0));
+                V[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, 0));
+                ge = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oe, 0, 0);
+                go = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oo, 0, 0);
+            }
             float ixe, iye, ite, ixo, iyo, ito;
             unpack_grad(ge, ixe, iye, ite);
             unpack_grad(go, ixo, iyo, ito);
@@ -674,12 +693,20 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
     for (int r = 0; r < RW; ++r) {
         const int wr = wv * RW + r;  // workgroup region row (wave-uniform)
         const bool rin = wr >= HL && wr < HL + OY && ((rowmask >> r) & 1ull);
-        const int oe = (rin && st_lane && ce) ? off0 + r * cols * 4 : kOOB;
-        const int oo = (rin && st_lane && co) ? off0 + r * cols * 4 + 4 : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].x), uo_rs, oe, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].y), uo_rs, oo, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].x), vo_rs, oe, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, oo, 0, 0);
+        if constexpr (!EDGE) {
+            const int o = (rin && st_lane) ? off0 + r * cols * 4 : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b64(
+                u2v{__float_as_uint(U[r].x), __float_as_uint(U[r].y)}, uo_rs, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(
+                u2v{__float_as_uint(V[r].x), __float_as_uint(V[r].y)}, vo_rs, o, 0, 0);
+        } else {
+            const int oe = (rin && st_lane && ce) ? off0 + r * cols * 4 : kOOB;
+            const int oo = (rin && st_lane && co) ? off0 + r * cols * 4 + 4 : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].x), uo_rs, oe, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].y), uo_rs, oo, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].x), vo_rs, oe, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, oo, 0, 0);
+        }
     }
 }
 

@@ -47,7 +47,8 @@ EXPORTS = (
     "hsflow_jacobi_device", "hsflow_set_iters_per_launch", "hsflow_iters_per_launch",
     "hsflow_bgr_to_gray", "hsflow_synth_pair", "hsflow_set_max_streams",
     "hsflow_pyramid_level_size", "hsflow_pyramid_workspace_bytes",
-    "hsflow_flow_pyramid_device", "hsflow_flow_pyramid",
+    "hsflow_flow_pyramid_device", "hsflow_flow_pyramid", "hsflow_bgr_to_gray_device",
+    "hsflow_flow_bgr",
 )
 
 
@@ -111,6 +112,9 @@ def lib():
                                              ctypes.c_float, _vp, _vp, _vp, _sz, _vp]
     L.hsflow_flow_pyramid.argtypes = [_vp, _vp, _vp, i, i, i, _sz, i, i, i,
                                       ctypes.c_double, _vp, _vp, i, _sz]
+    L.hsflow_bgr_to_gray_device.argtypes = [_vp, i, i, i, _vp, _vp]
+    L.hsflow_flow_bgr.argtypes = [_vp, _vp, _vp, i, i, _sz, i, i, ctypes.c_double, _vp,
+                                  _vp, i, _sz]
     L.hsflow_bgr_to_gray.argtypes = [_vp, i, i, _sz, _vp, _sz]
     L.hsflow_synth_pair.argtypes = [ctypes.c_uint64, i, i, i, i, _vp, _vp, _vp, _vp]
     _lib = L
@@ -207,6 +211,29 @@ class Context:
                                        _dtype_code(a), rows, cols, a.strides[0],
                                        int(levels), int(window), int(iters), float(alpha),
                                        u.ctypes.data, v.ctypes.data, code, u.strides[0])
+        _check(rc, self._p)
+        return u, v
+
+    def flow_bgr(self, bgr0, bgr1, window: int, iters: int, alpha: float,
+                 out_dtype=np.float64):
+        """main.cpp:50-51 + :13-14 + :97-98: decoded 8-bit BGR frames are
+        uploaded as BGR and converted to gray on the GPU, then solved."""
+        a = np.asarray(bgr0)
+        b = np.asarray(bgr1)
+        for x in (a, b):
+            if x.dtype != np.uint8 or x.ndim != 3 or x.shape[2] != 3:
+                raise HsflowError(HSFLOW_ERR_ARG, "need H x W x 3 BGR uint8")
+        if a.shape != b.shape:
+            raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
+        if a.strides[1:] != (3, 1) or b.strides[0] != a.strides[0]:
+            a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+        rows, cols = a.shape[:2]
+        u = np.empty((rows, cols), out_dtype)
+        v = np.empty((rows, cols), out_dtype)
+        code = F64 if u.dtype == np.float64 else F32
+        rc = lib().hsflow_flow_bgr(self._p, a.ctypes.data, b.ctypes.data, rows, cols,
+                                   a.strides[0], int(window), int(iters), float(alpha),
+                                   u.ctypes.data, v.ctypes.data, code, u.strides[0])
         _check(rc, self._p)
         return u, v
 
@@ -418,6 +445,21 @@ def bgr_to_gray(bgr) -> np.ndarray:
     _check(lib().hsflow_bgr_to_gray(bgr.ctypes.data, rows, cols, bgr.strides[0],
                                     out.ctypes.data, out.strides[0]))
     return out
+
+
+def bgr_to_gray_device(bgr, gray=None, stream=None):
+    """Device BGR->gray (same integer formula) on a uint8 CUDA tensor
+    [..., H, W, 3] -> [..., H, W].  Stream-ordered."""
+    if bgr.dtype != torch.uint8 or bgr.dim() < 3 or bgr.shape[-1] != 3 or \
+            not bgr.is_cuda or not bgr.is_contiguous():
+        raise HsflowError(HSFLOW_ERR_ARG, "need a contiguous uint8 CUDA tensor [..., H, W, 3]")
+    rows, cols = bgr.shape[-3], bgr.shape[-2]
+    batch = int(np.prod(bgr.shape[:-3])) if bgr.dim() > 3 else 1
+    if gray is None:
+        gray = torch.empty(bgr.shape[:-1], dtype=torch.uint8, device=bgr.device)
+    _check(lib().hsflow_bgr_to_gray_device(bgr.data_ptr(), rows, cols, batch,
+                                           gray.data_ptr(), _stream_ptr(stream)))
+    return gray
 
 
 def synth_pair(seed: int, rows: int, cols: int, qdy: int = -3, qdx: int = 6,

@@ -159,6 +159,18 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
 int hsflow_bgr_to_gray(const uint8_t *bgr, int rows, int cols, size_t bgr_step,
                        uint8_t *gray, size_t gray_step);
 
+/* The same conversion on the device (stream-ordered): `batch` dense BGR
+ * planes [batch][rows][cols][3] -> dense gray [batch][rows][cols]. */
+int hsflow_bgr_to_gray_device(const uint8_t *bgr, int rows, int cols, int batch,
+                              uint8_t *gray, void *stream);
+
+/* main.cpp:50-51 + :13-14 + :97-98 in one call: two decoded 8-bit BGR frames
+ * (row step bgr_step bytes) are uploaded as BGR, converted on the GPU and
+ * solved (hornSchunck::getFlow); u/v as in hsflow_flow. */
+int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, int rows,
+                    int cols, size_t bgr_step, int window, int iters, double alpha,
+                    void *u, void *v, int dtype_out, size_t out_step);
+
 /* Deterministic synthetic frame pair: I0 = smoothed hash noise
  * around 128 (integer-valued 0..255), I1 = I0's texture shifted by
  * (dy, dx) = (qdy/4, qdx/4) px with integer bilinear weights.  Outputs are
