@@ -422,7 +422,7 @@ __device__ __forceinline__ void hsum_c2(float ue, float uo, float ve, float vo, 
     }
 }
 
-template <int W, int KB, int RW, int NW, int SB, bool EDGE>
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[2][NW][W - 1][2][64], int tx,
                                         int ty, int wv, int lane, size_t pbase,
@@ -482,18 +482,27 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
 
     // interior workgroup: region + halo entirely inside the image, so no
     // border masks (wave-uniform; the masked body handles the rest)
-    // interior: the whole region lies inside the image, and rows are 8-byte
-    // aligned (even width) so the column pairs move as single 8-byte words
+    // For an even image width every lane's column pair (even first column)
+    // is 8-byte aligned and lies wholly inside or wholly outside the image,
+    // so it moves as one 8-byte word (fully coalesced 512 B per wave
+    // instruction instead of two half-line stride-2 dword accesses).  Odd
+    // widths take per-column dword accesses.
     const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols &&
-                          ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows &&
-                          (cols & 1) == 0;
-    if (interior)
-        wg_body<W, KB, RW, NW, SB, false>(p, xch, tx, ty, wv, lane, pbase, plane_bytes);
-    else
-        wg_body<W, KB, RW, NW, SB, true>(p, xch, tx, ty, wv, lane, pbase, plane_bytes);
+                          ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows;
+    if ((cols & 1) == 0) {
+        if (interior)
+            wg_body<W, KB, RW, NW, SB, false, true>(p, xch, tx, ty, wv, lane, pbase,
+                                                    plane_bytes);
+        else
+            wg_body<W, KB, RW, NW, SB, true, true>(p, xch, tx, ty, wv, lane, pbase,
+                                                   plane_bytes);
+    } else {
+        wg_body<W, KB, RW, NW, SB, true, false>(p, xch, tx, ty, wv, lane, pbase,
+                                                plane_bytes);
+    }
 }
 
-template <int W, int KB, int RW, int NW, int SB, bool EDGE>
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[2][NW][W - 1][2][64], int tx,
                                         int ty, int wv, int lane, size_t pbase,
@@ -543,11 +552,9 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
             uint32_t ge, go;
-            if constexpr (!EDGE) {
-                // interior tile of an even-width image: the lane's column
-                // pair is one aligned 8-byte word -> fully coalesced 512 B
-                // per wave instruction (vs two half-line stride-2 loads)
-                const int o = off0 + r * cols * 4;
+            if constexpr (X2) {
+                const int o = (!EDGE || (((rowmask >> r) & 1ull) && ce))
+                                  ? off0 + r * cols * 4 : kOOB;
                 const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, 0);
                 const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, 0);
                 const u2v g = __builtin_amdgcn_raw_buffer_load_b64(g_rs, o, 0, 0);
@@ -693,8 +700,8 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
     for (int r = 0; r < RW; ++r) {
         const int wr = wv * RW + r;  // workgroup region row (wave-uniform)
         const bool rin = wr >= HL && wr < HL + OY && ((rowmask >> r) & 1ull);
-        if constexpr (!EDGE) {
-            const int o = (rin && st_lane) ? off0 + r * cols * 4 : kOOB;
+        if constexpr (X2) {
+            const int o = (rin && st_lane && ce) ? off0 + r * cols * 4 : kOOB;
             __builtin_amdgcn_raw_buffer_store_b64(
                 u2v{__float_as_uint(U[r].x), __float_as_uint(U[r].y)}, uo_rs, o, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b64(
