@@ -12,11 +12,14 @@ solves its own pairs: weak scaling, no data-path collective (the timing
 barrier and max-over-ranks reduction are the only collectives).
 
 Rank 0 prints ONE JSON line.  Besides the driver fields it carries
-  roofline      dominant kernel (K2, hs_jacobi_kernel) measured live with
-                events on the launch stream; algorithmic bytes per launch are
-                the compulsory HBM bytes of one temporally-blocked pass
-                (DESIGN.md "Roofline"), traffic = PMC-measured bytes from the
-                committed rocprofv3 summary under profiles/ (or null)
+  roofline      dominant kernel (K2, hs_jacobi_wg_kernel) measured live with
+                events on the launch stream; achieved = SURVEY §8(d)'s 28 B
+                per pixel-iteration x the pixel-iterations of one launch /
+                launch time (> peak is possible: temporal blocking does KB
+                iterations per HBM pass); compulsory_* = the 20 B/px one
+                blocked pass must move, which PMC `traffic` (committed
+                rocprofv3 summary under profiles/, or null) is compared with
+                (DESIGN.md "Roofline")
   cpu_baseline  the float64 CPU port (oracle/, mirrors hornSchunck.cpp pass
                 by pass) on a bounded sample, 1 thread, rank 0 only
 """
@@ -165,12 +168,18 @@ def main():
     hsflow.set_max_streams(0)
     k2_ms = ev0.elapsed_time(ev1) / (reps * launches_per_solve)
     n_px = batch * px
-    # compulsory bytes of one blocked pass: read u, v (f32) + packed gradients
-    # (4 B) + write u, v; the first pass of a solve reads no u, v
-    first_frac = 1.0 / launches_per_solve
-    bytes_per_launch = n_px * (8 + 4 + 8 - 8 * first_frac)
+    # algorithmic bytes = 28 B per pixel-iteration (read u, v,
+    # Ix, Iy, It; write u', v' in f32) x the pixel-iterations one launch
+    # performs -- fixed by the algorithm, whatever the blocking saves
+    px_iters_per_launch = n_px * iters / launches_per_solve
+    bytes_per_launch = 28.0 * px_iters_per_launch
     achieved = bytes_per_launch / (k2_ms * 1e-3) / 1e9
-    jacobi_equiv = 28.0 * n_px * kb / (k2_ms * 1e-3) / 1e9  # SURVEY §8d 28 B/px*iter
+    # the HBM bytes one temporally-blocked pass cannot avoid (what the PMC
+    # traffic is compared with): read u, v (f32) + packed gradients (4 B),
+    # write u, v; the first pass of a solve reads no u, v
+    first_frac = 1.0 / launches_per_solve
+    compulsory = n_px * (8 + 4 + 8 - 8 * first_frac)
+    compulsory_gbps = compulsory / (k2_ms * 1e-3) / 1e9
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
@@ -212,8 +221,12 @@ def main():
                          "traffic": traffic,
                          "kernel": "hs_jacobi_wg_kernel",
                          "avg_launch_ms": round(k2_ms, 5),
+                         "iters_per_launch": kb,
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "jacobi_equiv_GBps_28B": round(jacobi_equiv, 1)},
+                         "algorithmic_B_per_px_iter": 28,
+                         "compulsory_bytes_per_launch": int(compulsory),
+                         "compulsory_GBps": round(compulsory_gbps, 1),
+                         "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4)},
             "cpu_baseline": cpu,
             "sane": ok,
         }

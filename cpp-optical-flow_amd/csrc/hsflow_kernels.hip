@@ -422,7 +422,7 @@ __device__ __forceinline__ void hsum_c2(float ue, float uo, float ve, float vo, 
     }
 }
 
-template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2>
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[2][NW][W - 1][2][64], int tx,
                                         int ty, int wv, int lane, size_t pbase,
@@ -459,50 +459,41 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)cols;
     const int plane_bytes = p.rows * cols * 4;
 
-    const uint32_t flag = p.flags != nullptr ? p.flags[pair] : 0u;
-    if (flag != 0u) {
-        // non-integral inputs: cover this workgroup's output tile with the
-        // f32-gradient regions of K2 (64 x 24, one wave each); no barriers
-        if constexpr (kb_ok_f32(W, KB)) {
-            constexpr int HLf = KB * A;
-            constexpr int OXf = 64 - KB * (W - 1), OYf = kRowsF32 - KB * (W - 1);
-            const int ox0 = tx * OX, oy0 = ty * OY;
-            constexpr int nsx = (OX + OXf - 1) / OXf, nsy = (OY + OYf - 1) / OYf;
-            for (int sidx = wv; sidx < nsx * nsy; sidx += NW) {
-                const int sy = sidx / nsx, sx = sidx - sy * nsx;
-                const int cx = ox0 + sx * OXf, cy = oy0 + sy * OYf;
-                jacobi_region<W, KB, kRowsF32, false>(p, pbase, plane_bytes, lane,
-                                                      cx - HLf + lane, cy - HLf,
-                                                      min(OYf, OY - sy * OYf),
-                                                      min(OXf, OX - sx * OXf));
-            }
-        }
-        return;
-    }
-
     // interior workgroup: region + halo entirely inside the image, so no
-    // border masks (wave-uniform; the masked body handles the rest)
+    // border masks (wave-uniform; the masked body handles the rest).
     // For an even image width every lane's column pair (even first column)
     // is 8-byte aligned and lies wholly inside or wholly outside the image,
     // so it moves as one 8-byte word (fully coalesced 512 B per wave
     // instruction instead of two half-line stride-2 dword accesses).  Odd
-    // widths take per-column dword accesses.
+    // widths take per-column dword accesses.  Pairs K1 flagged as
+    // non-integral read the f32 gradient planes instead of the packed words
+    // (same tiles, same operator, any blocking depth).
     const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols &&
                           ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows;
+    const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
+    if (g32) {
+        if ((cols & 1) == 0)
+            wg_body<W, KB, RW, NW, SB, true, true, true>(p, xch, tx, ty, wv, lane, pbase,
+                                                         plane_bytes);
+        else
+            wg_body<W, KB, RW, NW, SB, true, false, true>(p, xch, tx, ty, wv, lane, pbase,
+                                                          plane_bytes);
+        return;
+    }
     if ((cols & 1) == 0) {
         if (interior)
-            wg_body<W, KB, RW, NW, SB, false, true>(p, xch, tx, ty, wv, lane, pbase,
-                                                    plane_bytes);
+            wg_body<W, KB, RW, NW, SB, false, true, false>(p, xch, tx, ty, wv, lane, pbase,
+                                                           plane_bytes);
         else
-            wg_body<W, KB, RW, NW, SB, true, true>(p, xch, tx, ty, wv, lane, pbase,
-                                                   plane_bytes);
+            wg_body<W, KB, RW, NW, SB, true, true, false>(p, xch, tx, ty, wv, lane, pbase,
+                                                          plane_bytes);
     } else {
-        wg_body<W, KB, RW, NW, SB, true, false>(p, xch, tx, ty, wv, lane, pbase,
-                                                plane_bytes);
+        wg_body<W, KB, RW, NW, SB, true, false, false>(p, xch, tx, ty, wv, lane, pbase,
+                                                       plane_bytes);
     }
 }
 
-template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2>
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[2][NW][W - 1][2][64], int tx,
                                         int ty, int wv, int lane, size_t pbase,
@@ -532,8 +523,14 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
     const auto v_rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(p.v_in ? p.v_in + pbase : p.v_out + pbase), 0, p.v_in ? nbytes : 0,
         0x00020000);
-    const auto g_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gpack + pbase), 0,
-                                                        nbytes, 0x00020000);
+    const auto gp_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gpack + pbase), 0,
+                                                         G32 ? 0 : nbytes, 0x00020000);
+    const auto gx_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gx + pbase), 0,
+                                                         G32 ? nbytes : 0, 0x00020000);
+    const auto gy_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gy + pbase), 0,
+                                                         G32 ? nbytes : 0, 0x00020000);
+    const auto gt_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gt + pbase), 0,
+                                                         G32 ? nbytes : 0, 0x00020000);
 
     // (even, odd) column pairs as 2-wide vectors: the identical per-column
     // arithmetic issues as packed FP32 (v_pk_add/mul/fma_f32), one
@@ -551,17 +548,26 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
         const int off0 = (r0 * cols + gce) * 4;
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-            uint32_t ge, go;
+            float ixe, iye, ite, ixo, iyo, ito;
             if constexpr (X2) {
                 const int o = (!EDGE || (((rowmask >> r) & 1ull) && ce))
                                   ? off0 + r * cols * 4 : kOOB;
                 const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, 0);
                 const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, 0);
-                const u2v g = __builtin_amdgcn_raw_buffer_load_b64(g_rs, o, 0, 0);
                 U[r] = f2v{__uint_as_float(a.x), __uint_as_float(a.y)};
                 V[r] = f2v{__uint_as_float(b.x), __uint_as_float(b.y)};
-                ge = g.x;
-                go = g.y;
+                if constexpr (G32) {
+                    const u2v gx2 = __builtin_amdgcn_raw_buffer_load_b64(gx_rs, o, 0, 0);
+                    const u2v gy2 = __builtin_amdgcn_raw_buffer_load_b64(gy_rs, o, 0, 0);
+                    const u2v gt2 = __builtin_amdgcn_raw_buffer_load_b64(gt_rs, o, 0, 0);
+                    ixe = __uint_as_float(gx2.x); ixo = __uint_as_float(gx2.y);
+                    iye = __uint_as_float(gy2.x); iyo = __uint_as_float(gy2.y);
+                    ite = __uint_as_float(gt2.x); ito = __uint_as_float(gt2.y);
+                } else {
+                    const u2v g = __builtin_amdgcn_raw_buffer_load_b64(gp_rs, o, 0, 0);
+                    unpack_grad(g.x, ixe, iye, ite);
+                    unpack_grad(g.y, ixo, iyo, ito);
+                }
             } else {
                 const bool rin = (rowmask >> r) & 1ull;
                 const int oe = (rin && ce) ? off0 + r * cols * 4 : kOOB;
@@ -570,12 +576,20 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                 U[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, 0));
                 V[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, 0));
                 V[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, 0));
-                ge = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oe, 0, 0);
-                go = __builtin_amdgcn_raw_buffer_load_b32(g_rs, oo, 0, 0);
+                if constexpr (G32) {
+                    ixe = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gx_rs, oe, 0, 0));
+                    ixo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gx_rs, oo, 0, 0));
+                    iye = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gy_rs, oe, 0, 0));
+                    iyo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gy_rs, oo, 0, 0));
+                    ite = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gt_rs, oe, 0, 0));
+                    ito = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gt_rs, oo, 0, 0));
+                } else {
+                    unpack_grad(__builtin_amdgcn_raw_buffer_load_b32(gp_rs, oe, 0, 0), ixe,
+                                iye, ite);
+                    unpack_grad(__builtin_amdgcn_raw_buffer_load_b32(gp_rs, oo, 0, 0), ixo,
+                                iyo, ito);
+                }
             }
-            float ixe, iye, ite, ixo, iyo, ito;
-            unpack_grad(ge, ixe, iye, ite);
-            unpack_grad(go, ixo, iyo, ito);
             const float se = __builtin_amdgcn_rsqf(p.alpha2 + ixe * ixe + iye * iye);
             const float so = __builtin_amdgcn_rsqf(p.alpha2 + ixo * ixo + iyo * iyo);
             X[r] = f2v{ixe * se, ixo * so};
@@ -618,25 +632,26 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
 
         // 2. sweep slab rows t = -A .. RW+AR-1 through a ring of horizontal
         //    sums (hu, hv) and vertical pair sums q(t) = h(t) + h(t+1)
+        // Rows beyond the workgroup region (above wave 0, below wave NW-1)
+        // may hold anything finite or not: their influence moves A (AR)
+        // rows per iteration, so after KB iterations it has reached only
+        // the HL (HR) halo rows, which are never stored; at the image border
+        // those rows are re-zeroed every iteration (EDGE).  So the reads are
+        // unconditional, from a clamped slab (no branches, no zero fill).
+        const int wa = wv > 0 ? wv - 1 : 0, wb = wv < NW - 1 ? wv + 1 : NW - 1;
         f2v hu[W], hv[W], qu[W], qv[W];
 #pragma unroll
         for (int rr = 0; rr < RW + NB; ++rr) {
             const int t = rr - A;
             const int sl = (t + 2 * W) % W;
-            if (t < 0) {  // the slab above's bottom rows (zero above the region)
-                float2 a = make_float2(0.f, 0.f), b = make_float2(0.f, 0.f);
-                if (wv > 0) {
-                    a = xch[par][wv - 1][AR + (t + A)][0][lane];
-                    b = xch[par][wv - 1][AR + (t + A)][1][lane];
-                }
+            if (t < 0) {  // the slab above's bottom rows
+                const float2 a = xch[par][wa][AR + (t + A)][0][lane];
+                const float2 b = xch[par][wa][AR + (t + A)][1][lane];
                 hu[sl] = f2v{a.x, a.y};
                 hv[sl] = f2v{b.x, b.y};
             } else if (t >= RW) {  // the slab below's top rows
-                float2 a = make_float2(0.f, 0.f), b = make_float2(0.f, 0.f);
-                if (wv < NW - 1) {
-                    a = xch[par][wv + 1][t - RW][0][lane];
-                    b = xch[par][wv + 1][t - RW][1][lane];
-                }
+                const float2 a = xch[par][wb][t - RW][0][lane];
+                const float2 b = xch[par][wb][t - RW][1][lane];
                 hu[sl] = f2v{a.x, a.y};
                 hv[sl] = f2v{b.x, b.y};
             } else if (t < AR) {
@@ -791,9 +806,28 @@ static hipError_t launch_jacobi_t(JacobiArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Temporal-blocking depth per window: largest KB in {1,2,4,8} whose halo fits
-// 16 columns.  Overridable through hsflow_set_iters_per_launch().
+// K2 variant (HSFLOW_K2 env, diagnostics): 0 = per-wave regions
+// (hs_jacobi_kernel) for every window; otherwise the workgroup kernel.
+static int k2_variant() {
+    static int v = [] {
+        const char *e = getenv("HSFLOW_K2");
+        return e ? atoi(e) : 88;
+    }();
+    return v;
+}
+
+static bool uses_wg_kernel(int W) { return (W == 3 || W == 5) && k2_variant() != 0; }
+
+// Temporal-blocking depth per window (overridable through
+// hsflow_set_iters_per_launch).  The workgroup kernel (W = 3, 5) takes
+// KB in {1..6, 8} for packed and f32 gradients alike; its halo KB(W-1)
+// must leave at least half the 128 x 64 region as output.  The per-wave
+// kernel keeps the older limits (f32 regions are 24 rows).
 int default_kb(int W) {
+    // measured on MI355X (scripts/sweep.py, profiles/README.md): the extra
+    // halo work of deeper blocking is cheaper than the HBM pass it saves up
+    // to KB(W-1) = 24 for W = 5 and 16 for W = 3 (10/12/16 measured, no gain)
+    if (uses_wg_kernel(W)) return W == 3 ? 8 : 6;
     if (W < 1 || W > 9) return 1;
     for (int kb : {8, 4, 2})
         if (kb_ok_f32(W, kb)) return kb;
@@ -801,6 +835,8 @@ int default_kb(int W) {
 }
 
 bool kb_supported(int W, int KB, bool need_f32) {
+    if (uses_wg_kernel(W))
+        return ((KB >= 1 && KB <= 6) || KB == 8) && KB * (W - 1) <= 32;
     if (W < 1 || W > 9) return KB == 1;
     if (KB != 1 && KB != 2 && KB != 4 && KB != 8) return false;
     return need_f32 ? kb_ok_f32(W, KB) : kb_ok_packed(W, KB);
@@ -826,25 +862,16 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// K2 variant (tuning; HSFLOW_K2 env): 0 = per-wave regions (hs_jacobi_kernel);
-// otherwise the workgroup kernel with slab rows RW and NW stacked waves:
-// 88 -> (8, 8) default, 816 -> (8, 16), 128 -> (12, 8), 164 -> (16, 4).
-static int k2_variant() {
-    static int v = [] {
-        const char *e = getenv("HSFLOW_K2");
-        return e ? atoi(e) : 88;
-    }();
-    return v;
-}
 
 template <int W, int KB>
 static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
-    switch (k2_variant()) {
-    case 816: return launch_jacobi_wg<W, KB, 8, 16, 1>(a, s);
-    case 128: return launch_jacobi_wg<W, KB, 12, 8, 1>(a, s);
-    case 164: return launch_jacobi_wg<W, KB, 16, 4, 1>(a, s);
-    default: return launch_jacobi_wg<W, KB, 8, 8, 1>(a, s);
-    }
+    // 8 waves x 8 slab rows (64 x 128 region).  Measured alternatives, all
+    // slower on MI355X: 16 x 8 (one workgroup per CU), 8 x 12 and 4 x 16
+    // (VGPR spills).  SB = 16 > rows swept: no scheduling barriers inside
+    // the sweep (110 VGPRs, no spills; the scheduler interleaves rows and
+    // fills the DPP read-after-write wait states: 10 s_nop per iteration
+    // instead of 23).
+    return launch_jacobi_wg<W, KB, 8, 8, 16>(a, s);
 }
 
 template <int W>
@@ -854,7 +881,10 @@ static hipError_t launch_jacobi_w(JacobiArgs a, int KB, hipStream_t s) {
             switch (KB) {
             case 1: return launch_jacobi_wgv<W, 1>(a, s);
             case 2: return launch_jacobi_wgv<W, 2>(a, s);
+            case 3: return launch_jacobi_wgv<W, 3>(a, s);
             case 4: return launch_jacobi_wgv<W, 4>(a, s);
+            case 5: return launch_jacobi_wgv<W, 5>(a, s);
+            case 6: return launch_jacobi_wgv<W, 6>(a, s);
             case 8: return launch_jacobi_wgv<W, 8>(a, s);
             default: return hipErrorInvalidValue;
             }

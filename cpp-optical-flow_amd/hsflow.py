@@ -28,7 +28,8 @@ except Exception:  # pragma: no cover - torch is optional for the host API
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhsflow.so")
+# HSFLOW_LIB: load another build of the library (same-box A/B timing only)
+LIB_PATH = os.environ.get("HSFLOW_LIB") or os.path.join(_HERE, "libhsflow.so")
 
 HSFLOW_OK = 0
 HSFLOW_ERR_ARG = -1
