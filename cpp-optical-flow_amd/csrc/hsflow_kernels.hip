@@ -865,13 +865,15 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
 
 template <int W, int KB>
 static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
-    // 8 waves x 8 slab rows (64 x 128 region).  Measured alternatives, all
-    // slower on MI355X: 16 x 8 (one workgroup per CU), 8 x 12 and 4 x 16
-    // (VGPR spills).  SB = 16 > rows swept: no scheduling barriers inside
-    // the sweep (110 VGPRs, no spills; the scheduler interleaves rows and
-    // fills the DPP read-after-write wait states: 10 s_nop per iteration
-    // instead of 23).
-    return launch_jacobi_wg<W, KB, 8, 8, 16>(a, s);
+    // 8 waves x 10 slab rows (80 x 128 region, 128 VGPRs, no spills).
+    // Same-box A/B on MI355X (scripts/ab_bench.sh), W = 5, KB = 6:
+    // 8 rows 820k / 941k, 9 rows 850k / 995k, 10 rows 863k / 1026k
+    // Mpix*iter/s at 1080p / 4K (the taller slab shrinks the share of
+    // temporal-halo rows).  Also slower: 16 waves x 8 rows (one workgroup
+    // per CU).  SB = 16 > rows swept: no scheduling barriers inside the
+    // sweep, so the scheduler interleaves rows and fills the DPP
+    // read-after-write wait states.
+    return launch_jacobi_wg<W, KB, 10, 8, 16>(a, s);
 }
 
 template <int W>
