@@ -65,10 +65,14 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=0,
                     help="Jacobi iterations of the CPU sample (0: auto ~15 s)")
     ap.add_argument("--roofline-reps", type=int, default=3)
-    ap.add_argument("--mode", choices=["resident", "stream"], default="resident",
+    ap.add_argument("--mode", choices=["resident", "stream", "bands"], default="resident",
                     help="resident: pairs generated on each rank, already in HBM "
                          "(the metric); stream: BASELINE config 4, rank 0 holds "
-                         "--pairs pairs and scatters/gathers them over RCCL")
+                         "--pairs pairs and scatters/gathers them over RCCL; bands: "
+                         "BASELINE config 5 on N GPUs, ONE pair split into row bands "
+                         "with a halo exchange (row_bands.py)")
+    ap.add_argument("--chunk", type=int, default=12,
+                    help="bands mode: iterations between halo exchanges")
     ap.add_argument("--pairs", type=int, default=64, help="stream mode: pairs in the stream")
     return ap.parse_args()
 
@@ -91,6 +95,8 @@ def main():
 
     if args.mode == "stream":
         return stream_mode(args, world, rank, dev)
+    if args.mode == "bands":
+        return bands_mode(args, world, rank, dev)
 
     wl = dict(WORKLOADS[args.workload])
     rows, cols = wl["rows"], wl["cols"]
@@ -292,6 +298,76 @@ def stream_mode(args, world, rank, dev):
                        "pairs": n, "iters": iters, "window": args.window,
                        "parallelism": f"frame-parallel x{world}"},
             "Mpix_iter_per_s": round(total * rows * cols * iters / elapsed / 1e6, 1),
+            "sane": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bands_mode(args, world, rank, dev):
+    """BASELINE config 5 across ranks: one pair (default the 8k workload,
+    fp16, 3 levels) split into row bands; every `--chunk` iterations each
+    rank exchanges halo rows with its neighbours over RCCL, and rank 0
+    gathers (u, v).  Timed: pyramid build + banded levels + exchanges +
+    gather (inputs broadcast from rank 0 beforehand, resident in HBM).
+    Strong scaling: the work is fixed, value = pair Mpix*iter/s."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import hsflow
+    import row_bands as rb
+
+    wl = dict(WORKLOADS[args.workload if args.workload != "1080p" else "8k"])
+    rows, cols = wl["rows"], wl["cols"]
+    iters = args.iters or wl["iters"]
+    levels = args.levels or wl.get("levels", 1)
+    in_dtype = args.dtype or wl.get("dtype", "f32")
+    tdt = {"f16": torch.float16, "f32": torch.float32, "u8": torch.uint8}[in_dtype]
+    I0 = torch.empty((rows, cols), dtype=tdt, device=dev)
+    I1 = torch.empty_like(I0)
+    if rank == 0:
+        a, b = hsflow.synth_pair(1000, rows, cols,
+                                 dtype=np.uint8 if in_dtype == "u8" else np.float32)
+        I0.copy_(torch.from_numpy(a).to(dev).to(tdt))
+        I1.copy_(torch.from_numpy(b).to(dev).to(tdt))
+    if world > 1:
+        dist.broadcast(I0, 0)
+        dist.broadcast(I1, 0)
+    p = rb.plan(rows, cols, levels, world, args.window, args.chunk)
+    ops = [rb.DeviceOps(args.window, args.alpha, dev)]
+    comm = rb.DistComm() if world > 1 else rb.LocalComm()
+
+    def one():
+        states = rb.solve([I0], [I1], p, iters, ops, comm, [rank])
+        return rb.gather_owned(states, p, comm)
+
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        u, v = one()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    px_all = sum(r * c for r, c in p.sizes)
+    if rank == 0:
+        ok = bool(torch.isfinite(u).all().item()) and 0.05 < float(u.mean()) < 0.3
+        print(json.dumps({
+            "metric": "Mpix*iter/s (config 5: one pair in row bands, halo exchange over RCCL)",
+            "value": round(px_all * iters * args.steps / elapsed / 1e6, 1),
+            "unit": "Mpix*iter/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32", "data": f"synthetic {in_dtype} frame pair",
+            "config": {"workload": f"{cols}x{rows}, {levels} levels, {iters} it/level",
+                       "window": args.window, "chunk": args.chunk, "halo_rows": p.halo,
+                       "parallelism": f"row bands x{world}"},
             "sane": ok}), flush=True)
     if world > 1:
         dist.destroy_process_group()

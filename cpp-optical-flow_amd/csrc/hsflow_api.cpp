@@ -695,6 +695,51 @@ size_t hsflow_pyramid_workspace_bytes(int rows, int cols, int batch, int levels)
     return pyr_layout(rows, cols, batch, levels).bytes;
 }
 
+int hsflow_pyramid_build_device(const void *I0, const void *I1, int dtype_in, int rows,
+                                int cols, int batch, int levels, float *const *I0_levels,
+                                float *const *I1_levels, void *workspace,
+                                size_t workspace_bytes, void *stream) {
+    if (levels < 1 || levels > HSFLOW_MAX_LEVELS)
+        return fail(nullptr, HSFLOW_ERR_ARG, "levels %d outside [1, %d]", levels,
+                    HSFLOW_MAX_LEVELS);
+    if (levels > 1 && (!I0_levels || !I1_levels))
+        return fail(nullptr, HSFLOW_ERR_ARG, "null level array");
+    for (int l = 1; l < levels; ++l)
+        if (!I0_levels[l - 1] || !I1_levels[l - 1])
+            return fail(nullptr, HSFLOW_ERR_ARG, "null level plane %d", l);
+    hipStream_t s = (hipStream_t)stream;
+    // K1 at level 0 decides each pair's rounding (flags in the workspace)
+    int rc = gradients_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, nullptr, nullptr,
+                            nullptr, workspace, workspace_bytes, s);
+    if (rc || levels == 1) return rc;
+    const uint32_t *flags = carve(workspace, rows, cols, batch).flags;
+    int r = rows, c = cols;
+    for (int l = 1; l < levels; ++l) {
+        for (int k = 0; k < 2; ++k) {
+            const void *src = l == 1 ? (k ? I1 : I0)
+                                     : (const void *)(k ? I1_levels[l - 2] : I0_levels[l - 2]);
+            hipError_t e = hsflow::launch_pyrdown(src, l == 1 ? dtype_in : HSFLOW_F32, r, c,
+                                                  batch, k ? I1_levels[l - 1] : I0_levels[l - 1],
+                                                  flags, s);
+            if (e != hipSuccess) return hip_fail(nullptr, e, "pyrdown launch");
+        }
+        r = (r + 1) / 2;
+        c = (c + 1) / 2;
+    }
+    return HSFLOW_OK;
+}
+
+int hsflow_upflow_device(const float *uc, const float *vc, int rc, int cc, float *u,
+                         float *v, int rows, int cols, int batch, void *stream) {
+    if (!uc || !vc || !u || !v) return fail(nullptr, HSFLOW_ERR_ARG, "null device pointer");
+    if (!sizes_ok(rows, cols, batch) || rc < (rows + 1) / 2 || cc < (cols + 1) / 2)
+        return fail(nullptr, HSFLOW_ERR_ARG, "bad sizes %dx%d from %dx%d", rows, cols, rc, cc);
+    hipError_t e = hsflow::launch_upflow(uc, vc, rc, cc, u, v, rows, cols, batch,
+                                         (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(nullptr, e, "upflow launch");
+    return HSFLOW_OK;
+}
+
 int hsflow_flow_pyramid_device(const void *I0, const void *I1, int dtype_in, int rows,
                                int cols, int batch, int levels, int window, int iters,
                                float alpha, float *u, float *v, void *workspace,

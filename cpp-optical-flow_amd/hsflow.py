@@ -49,7 +49,7 @@ EXPORTS = (
     "hsflow_bgr_to_gray", "hsflow_synth_pair", "hsflow_set_max_streams",
     "hsflow_pyramid_level_size", "hsflow_pyramid_workspace_bytes",
     "hsflow_flow_pyramid_device", "hsflow_flow_pyramid", "hsflow_bgr_to_gray_device",
-    "hsflow_flow_bgr",
+    "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
 )
 
 
@@ -113,6 +113,10 @@ def lib():
                                              ctypes.c_float, _vp, _vp, _vp, _sz, _vp]
     L.hsflow_flow_pyramid.argtypes = [_vp, _vp, _vp, i, i, i, _sz, i, i, i,
                                       ctypes.c_double, _vp, _vp, i, _sz]
+    L.hsflow_pyramid_build_device.argtypes = [_vp, _vp, i, i, i, i, i,
+                                              ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                              _vp, _sz, _vp]
+    L.hsflow_upflow_device.argtypes = [_vp, _vp, i, i, _vp, _vp, i, i, i, _vp]
     L.hsflow_bgr_to_gray_device.argtypes = [_vp, i, i, i, _vp, _vp]
     L.hsflow_flow_bgr.argtypes = [_vp, _vp, _vp, i, i, _sz, i, i, ctypes.c_double, _vp,
                                   _vp, i, _sz]
@@ -398,6 +402,40 @@ def flow_pyramid_device(I0, I1, levels: int, window: int, iters: int, alpha: flo
                                           workspace.numel(), _stream_ptr(stream))
     _check(rc)
     return u, v
+
+
+def pyramid_build_device(I0, I1, levels: int, workspace=None, stream=None):
+    """Levels 1..levels-1 of both frames (f32 tensors [B, h_l, w_l]), the
+    same planes hsflow_flow_pyramid_device builds internally."""
+    rows, cols = I0.shape[-2:]
+    batch = int(np.prod(I0.shape[:-2])) if I0.dim() > 2 else 1
+    _check_dense(I0, (rows, cols), "I0")
+    _check_dense(I1, (rows, cols), "I1")
+    lead = tuple(I0.shape[:-2])
+    P0, P1 = [], []
+    for l in range(1, levels):
+        r, c = pyramid_level_size(rows, cols, l)
+        P0.append(torch.empty(lead + (r, c), dtype=torch.float32, device=I0.device))
+        P1.append(torch.empty(lead + (r, c), dtype=torch.float32, device=I0.device))
+    if workspace is None:
+        workspace = alloc_workspace(rows, cols, batch, I0.device)
+    n = max(1, levels - 1)
+    a0 = (_vp * n)(*[t.data_ptr() for t in P0]) if P0 else (_vp * 1)()
+    a1 = (_vp * n)(*[t.data_ptr() for t in P1]) if P1 else (_vp * 1)()
+    _check(lib().hsflow_pyramid_build_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
+                                             rows, cols, batch, int(levels), a0, a1,
+                                             workspace.data_ptr(), workspace.numel(),
+                                             _stream_ptr(stream)))
+    return P0, P1
+
+
+def upflow_device(uc, vc, u, v, stream=None):
+    """u = 2 uc(y/2, x/2), v likewise (the pyramid's warm start); u, v and
+    uc, vc are dense [rows, cols] / [rc, cc] views (row slices allowed)."""
+    rc, cc = uc.shape[-2:]
+    rows, cols = u.shape[-2:]
+    _check(lib().hsflow_upflow_device(uc.data_ptr(), vc.data_ptr(), rc, cc, u.data_ptr(),
+                                      v.data_ptr(), rows, cols, 1, _stream_ptr(stream)))
 
 
 def gradients_device(I0, I1, workspace, gx=None, gy=None, gt=None, stream=None):

@@ -152,6 +152,21 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
                         int iters, double alpha, void *u, void *v, int dtype_out,
                         size_t out_step);
 
+/* The pyramid's pieces, for callers that schedule the levels themselves
+ * (e.g. cpp-optical-flow_amd/row_bands.py, one 8K pair split over GPUs):
+ * levels 1..levels-1 of both frames into caller planes I0_levels[l-1],
+ * I1_levels[l-1] (dense f32, batch x level size), rounding decided per pair
+ * exactly as hsflow_flow_pyramid_device does; `workspace` as for
+ * hsflow_workspace_bytes(rows, cols, batch)... */
+int hsflow_pyramid_build_device(const void *I0, const void *I1, int dtype_in, int rows,
+                                int cols, int batch, int levels, float *const *I0_levels,
+                                float *const *I1_levels, void *workspace,
+                                size_t workspace_bytes, void *stream);
+/* ...and the warm start of a finer level: u = 2 uc(y/2, x/2), v likewise
+ * (rows x cols from rc x cc, dense, batch planes). */
+int hsflow_upflow_device(const float *uc, const float *vc, int rc, int cc, float *u,
+                         float *v, int rows, int cols, int batch, void *stream);
+
 /* ---- host utilities on the path to the hot loop ------------------------ */
 
 /* main.cpp:13-14 cv::cvtColor(BGR2GRAY) for 8-bit BGR, OpenCV 4.x 15-bit

@@ -42,7 +42,7 @@ def test_workspace_bytes():
 
 
 def test_iters_per_launch_policy():
-    assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 4
+    assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 6  # measured default
     assert hsflow.iters_per_launch(1080, 1920, 1, 3) == 8
     assert hsflow.iters_per_launch(1080, 1920, 1, 12) == 1
     with pytest.raises(hsflow.HsflowError):

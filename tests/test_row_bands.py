@@ -1,0 +1,201 @@
+"""Config 5 split over ranks (cpp-optical-flow_amd/row_bands.py): one frame
+pair in row bands with a halo exchange after every chunk of iterations.
+
+The claim under test is exactness: every owned row equals the undivided
+solve bit for bit.  On CPU the band solver is the float64 oracle (test
+infrastructure) and the reference is oracle.flow_pyramid; the exchange runs
+both in-process (LocalComm) and over torch.distributed gloo with 2 and 3
+processes (DistComm, the code RCCL runs on the GPU box).  On the GPU the
+band solver is libhsflow and the reference hsflow.flow_pyramid_device."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+import row_bands as rb
+from synth_ref import synth_pair
+
+
+class OracleOps:
+    """The band operations restated with the float64 oracle pieces."""
+
+    def __init__(self, window, alpha):
+        self.window, self.alpha = window, alpha
+
+    def levels(self, I0, I1, L):
+        a, b = np.asarray(I0, np.float64), np.asarray(I1, np.float64)
+        rnd = oracle.integer_pair(a, b)
+        P0, P1 = [a], [b]
+        for _ in range(1, L):
+            P0.append(oracle.pyrdown(P0[-1], rnd))
+            P1.append(oracle.pyrdown(P1[-1], rnd))
+        return P0, P1
+
+    def zeros(self, r, c):
+        return np.zeros((r, c), np.float64)
+
+    def gradients(self, J0, J1):
+        return oracle.gradients(J0, J1)
+
+    def jacobi(self, g, u, v, n):
+        nu, nv = oracle.jacobi(g[0], g[1], g[2], u, v, self.window, n, self.alpha)
+        u[...] = nu
+        v[...] = nv
+
+    def upflow(self, uc, vc, u, v):
+        r, c = u.shape
+        u[...] = 2.0 * np.repeat(np.repeat(uc, 2, 0), 2, 1)[:r, :c]
+        v[...] = 2.0 * np.repeat(np.repeat(vc, 2, 0), 2, 1)[:r, :c]
+
+
+# ------------------------------------------------------------------ planning
+@pytest.mark.parametrize("rows,levels,world,chunk", [(4320, 3, 8, 12), (1080, 3, 4, 6),
+                                                     (97, 2, 3, 3), (64, 1, 2, 4)])
+def test_plan_bands_tile_and_nest(rows, levels, world, chunk):
+    p = rb.plan(rows, 77, levels, world, 5, chunk)
+    assert p.halo == chunk * 2 and p.halo % 2 == 0
+    for l, (R, _) in enumerate(p.sizes):
+        bands = p.bands[l]
+        assert bands[0].a == 0 and bands[-1].b == R
+        for x, y in zip(bands, bands[1:]):
+            assert x.b == y.a                               # owned rows tile the level
+        for k, bd in enumerate(bands):
+            assert bd.b - bd.a >= p.halo or world == 1
+            assert bd.e0 == (0 if k == 0 else bd.a - p.halo)
+            assert bd.e1 == (R if k == world - 1 else bd.b + p.halo)
+            if l < levels - 1:                              # levels warm-started from
+                assert bd.e0 % 2 == 0                       # a coarser one map rows exactly
+            if l > 0:
+                assert bd.a == p.bands[0][k].a >> l         # bands nest across levels
+
+
+def test_plan_rejects_bands_shorter_than_the_halo():
+    with pytest.raises(ValueError):
+        rb.plan(100, 50, 3, 8, 5, 12)
+
+
+# --------------------------------------------------- oracle-backed, one process
+def _pair(rows, cols, seed=1000):
+    return synth_pair(seed, rows, cols)
+
+
+@pytest.mark.parametrize("world,levels,chunk,window", [(2, 2, 3, 5), (3, 3, 2, 5),
+                                                       (4, 1, 2, 3)])
+def test_local_bands_equal_undivided_oracle(world, levels, chunk, window):
+    I0, I1 = _pair(70, 53)
+    iters = 7
+    p = rb.plan(70, 53, levels, world, window, chunk)
+    ops = [OracleOps(window, 1.0) for _ in range(world)]
+    comm = rb.LocalComm()
+    states = rb.solve([I0] * world, [I1] * world, p, iters, ops, comm, list(range(world)))
+    u, v = rb.gather_owned(states, p, comm)
+    uo, vo = oracle.flow_pyramid(I0, I1, levels, window, iters, 1.0)
+    assert np.array_equal(u, uo) and np.array_equal(v, vo)
+
+
+def test_local_bands_non_integral_frames():
+    I0, I1 = _pair(66, 41)
+    I0 = I0 * np.float32(0.7) + np.float32(0.2)
+    p = rb.plan(66, 41, 2, 2, 5, 3)
+    comm = rb.LocalComm()
+    states = rb.solve([I0] * 2, [I1] * 2, p, 5, [OracleOps(5, 1.0) for _ in range(2)], comm,
+                      [0, 1])
+    u, _ = rb.gather_owned(states, p, comm)
+    uo, _ = oracle.flow_pyramid(I0, I1, 2, 5, 5, 1.0)
+    assert np.array_equal(u, uo)
+
+
+# ------------------------------------------------------- gloo, several processes
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+ROWS, COLS, LEVELS, ITERS, CHUNK = 72, 45, 2, 8, 3
+
+
+def _worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [here, os.path.join(root, "oracle"), os.path.join(root, "cpp-optical-flow_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        I0, I1 = synth_pair(1000, ROWS, COLS)
+        p = rb.plan(ROWS, COLS, LEVELS, world, 5, CHUNK)
+        comm = rb.DistComm()
+        states = rb.solve([I0], [I1], p, ITERS, [OracleOps(5, 1.0)], comm, [rank])
+        u, v = rb.gather_owned(states, p, comm)
+        q.put(("ok", rank, None if u is None else (u.copy(), v.copy())))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_bands_equal_undivided_oracle(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+    errs = [r for r in res if r[0] == "err"]
+    assert not errs, errs
+    (out,) = [r[2] for r in res if r[1] == 0]
+    I0, I1 = synth_pair(1000, ROWS, COLS)
+    uo, vo = oracle.flow_pyramid(I0, I1, LEVELS, 5, ITERS, 1.0)
+    assert np.array_equal(out[0], uo) and np.array_equal(out[1], vo)
+
+
+
+# ----------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def hs():
+    import hsflow
+    return hsflow
+
+
+def _bands_on_one_gpu(hs, I0, I1, levels, window, iters, world, chunk, dtype=None):
+    t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
+    if dtype is not None:
+        t0, t1 = t0.to(dtype), t1.to(dtype)
+    rows, cols = I0.shape
+    p = rb.plan(rows, cols, levels, world, window, chunk)
+    ops = [rb.DeviceOps(window, 1.0, t0.device) for _ in range(world)]
+    comm = rb.LocalComm()
+    states = rb.solve([t0] * world, [t1] * world, p, iters, ops, comm, list(range(world)))
+    u, v = rb.gather_owned(states, p, comm)
+    ref = hs.flow_pyramid_device(t0, t1, levels, window, iters, 1.0)
+    torch.cuda.synchronize()
+    return (u, v), ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,levels,chunk,window", [(2, 3, 6, 5), (4, 2, 12, 5),
+                                                       (3, 3, 8, 3)])
+def test_device_bands_bit_identical_to_single_gpu(hs, world, levels, chunk, window):
+    I0, I1 = hs.synth_pair(1000, 400, 522)
+    (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, levels, window, 40, world, chunk)
+    assert torch.equal(u, ur) and torch.equal(v, vr)
+
+
+@pytest.mark.gpu
+def test_device_bands_8k_fp16_eight_ranks(hs):
+    """Config 5 geometry: 7680x4320 fp16, 3 levels, 8 bands, chunk 12."""
+    I0, I1 = hs.synth_pair(1000, 4320, 7680)
+    (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, 3, 5, 30, 8, 12, torch.float16)
+    assert torch.equal(u, ur) and torch.equal(v, vr)
