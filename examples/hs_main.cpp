@@ -2,7 +2,11 @@
 // MI355X solver, without OpenCV (PGM/PPM in, YAML + PPM out).
 //
 //   hs_main <prev.{pgm,ppm}> <next.{pgm,ppm}> <savePath> [windowSize maxIterations alpha]
+//   hs_main <video.y4m> <prevFrame> <nextFrame> <savePath> [windowSize maxIterations alpha]
 //
+// main.cpp:53-59   the video branch (VideoCapture + CAP_PROP_POS_FRAMES seek)
+//                  over YUV4MPEG2, the decoder-free raw container; gray =
+//                  luma, video range expanded to 0..255 (frames.Y4MVideo)
 // main.cpp:50-51   read the two frames (PPM = 8-bit RGB, PGM = 8-bit gray)
 // main.cpp:65-73   empty / size-mismatch checks -> return -1
 // main.cpp:84      preprocess: BGR -> gray, OpenCV 4.x 15-bit (hsflow_bgr_to_gray)
@@ -11,6 +15,7 @@
 //                  YAML layout ("u matrix" / "v matrix", !!opencv-matrix, dt: d)
 // main.cpp:103-104 plotFlow(prev raw).plotBresenhamLine(u, v, 20, 20, 5) ->
 //                  <savePath>hsbresenhamLineFlow.ppm (headless: no imshow)
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -60,6 +65,59 @@ bool read_pnm(const std::string &path, Image &im) {
     if (im.channels == 3)  // PPM stores RGB; imread gives BGR
         for (size_t i = 0; i < im.px.size(); i += 3) std::swap(im.px[i], im.px[i + 2]);
     return true;
+}
+
+// YUV4MPEG2 frame `index` as gray (see frames.py Y4MVideo for the rule)
+bool read_y4m_frame(const std::string &path, long index, Image &im) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f || index < 0) return false;
+    std::string head;
+    std::getline(f, head);
+    if (head.rfind("YUV4MPEG2", 0) != 0) return false;
+    std::istringstream hs(head);
+    std::string tok, cs = "420jpeg";
+    int w = 0, h = 0;
+    bool full = false;
+    while (hs >> tok) {
+        if (tok[0] == 'W') w = std::atoi(tok.c_str() + 1);
+        else if (tok[0] == 'H') h = std::atoi(tok.c_str() + 1);
+        else if (tok[0] == 'C') cs = tok.substr(1);
+        else if (tok == "XCOLORRANGE=FULL") full = true;
+    }
+    if (w <= 0 || h <= 0) return false;
+    size_t chroma = 0;
+    if (cs.rfind("mono", 0) != 0) {
+        int sx = 2, sy = 2;
+        if (cs.rfind("444", 0) == 0) sx = sy = 1;
+        else if (cs.rfind("422", 0) == 0) sy = 1;
+        else if (cs.rfind("411", 0) == 0) { sx = 4; sy = 1; }
+        chroma = 2 * (size_t)((w + sx - 1) / sx) * (size_t)((h + sy - 1) / sy);
+    }
+    const size_t luma = (size_t)w * h;
+    for (long i = 0;; ++i) {  // frame headers may carry parameters: walk them
+        std::string fh;
+        if (!std::getline(f, fh) || fh.rfind("FRAME", 0) != 0) return false;
+        if (i == index) break;
+        f.seekg((std::streamoff)(luma + chroma), std::ios::cur);
+    }
+    im.rows = h;
+    im.cols = w;
+    im.channels = 1;
+    im.px.resize(luma);
+    f.read((char *)im.px.data(), (std::streamsize)luma);
+    if (!f) return false;
+    if (!full)
+        for (auto &y : im.px) {
+            const int g = ((int)y - 16) * 255 + 109;
+            const int q = g >= 0 ? g / 219 : -((-g + 218) / 219);
+            y = (uint8_t)std::min(255, std::max(0, q));
+        }
+    return true;
+}
+
+bool ends_with(const std::string &s, const char *suf) {
+    const size_t n = std::strlen(suf);
+    return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
 }
 
 bool write_ppm_bgr(const std::string &path, const Image &im) {
@@ -170,16 +228,28 @@ void plot_bresenham_line(Image &im, const std::vector<double> &u, const std::vec
 int main(int argc, char **argv) {
     if (argc < 4) {
         std::cout << "usage: hs_main prev.{pgm,ppm} next.{pgm,ppm} savePath "
+                     "[windowSize maxIterations alpha]\n"
+                     "       hs_main video.y4m prevFrame nextFrame savePath "
                      "[windowSize maxIterations alpha]\n";
         return 0;
     }
-    const std::string savePath = argv[3];
-    const int windowSize = argc > 4 ? std::atoi(argv[4]) : 5;      // main.cpp:94
-    const int maxIterations = argc > 5 ? std::atoi(argv[5]) : 100;  // main.cpp:95
-    const double alpha = argc > 6 ? std::atof(argv[6]) : 1.0;       // main.cpp:96
+    // main.cpp:48-64: image pair or two frames of a video by index
+    const bool video = ends_with(argv[1], ".y4m");
+    if (video && argc < 5) {
+        std::cout << "No image or video input given! Please try again!" << std::endl;
+        return 0;
+    }
+    const int a0 = video ? 5 : 4;  // first optional argument
+    const std::string savePath = argv[a0 - 1];
+    const int windowSize = argc > a0 ? std::atoi(argv[a0]) : 5;          // main.cpp:94
+    const int maxIterations = argc > a0 + 1 ? std::atoi(argv[a0 + 1]) : 100;  // main.cpp:95
+    const double alpha = argc > a0 + 2 ? std::atof(argv[a0 + 2]) : 1.0;       // main.cpp:96
 
     Image prevRaw, nextRaw;
-    if (!read_pnm(argv[1], prevRaw) || !read_pnm(argv[2], nextRaw)) {
+    const bool ok = video ? read_y4m_frame(argv[1], std::atol(argv[2]), prevRaw) &&
+                                read_y4m_frame(argv[1], std::atol(argv[3]), nextRaw)
+                          : read_pnm(argv[1], prevRaw) && read_pnm(argv[2], nextRaw);
+    if (!ok) {
         std::cout << "Can't read the images. Please check the path." << std::endl;
         return -1;
     }
