@@ -628,7 +628,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
             xch[par][wv][AR + k][0][lane] = make_float2(hbu[k].x, hbu[k].y);
             xch[par][wv][AR + k][1][lane] = make_float2(hbv[k].x, hbv[k].y);
         }
-        __syncthreads();
+        if (p.ablate < 3) __syncthreads();  // 3/4: timing diagnostics only
 
         // 2. sweep slab rows t = -A .. RW+AR-1 through a ring of horizontal
         //    sums (hu, hv) and vertical pair sums q(t) = h(t) + h(t+1)
@@ -638,7 +638,8 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
         // the HL (HR) halo rows, which are never stored; at the image border
         // those rows are re-zeroed every iteration (EDGE).  So the reads are
         // unconditional, from a clamped slab (no branches, no zero fill).
-        const int wa = wv > 0 ? wv - 1 : 0, wb = wv < NW - 1 ? wv + 1 : NW - 1;
+        const int wa = p.ablate == 4 ? wv : (wv > 0 ? wv - 1 : 0);
+        const int wb = p.ablate == 4 ? wv : (wv < NW - 1 ? wv + 1 : NW - 1);
         f2v hu[W], hv[W], qu[W], qv[W];
 #pragma unroll
         for (int rr = 0; rr < RW + NB; ++rr) {
