@@ -195,9 +195,13 @@ def main():
         if pmc.get("kb") == kb and pmc.get("batch") == batch:
             traffic = pmc.get("hbm_bytes_per_launch")
 
-    cpu = None
+    cpu = cpu_all = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(rows, cols, args.window, args.alpha, args.cpu_iters)
+        # SURVEY §8(d) second CPU line: all cores of the box's CPU share
+        # (16 per GPU on the MI355X pool; os.cpu_count() shows the machine)
+        n_thr = min(16, os.cpu_count() or 1)
+        cpu_all = cpu_baseline(rows, cols, args.window, args.alpha, args.cpu_iters, n_thr)
 
     if rank == 0:
         line = {
@@ -234,6 +238,7 @@ def main():
                          "compulsory_GBps": round(compulsory_gbps, 1),
                          "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4)},
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
             "sane": ok,
         }
         print(json.dumps(line), flush=True)
@@ -373,24 +378,25 @@ def bands_mode(args, world, rank, dev):
         dist.destroy_process_group()
 
 
-def cpu_baseline(rows, cols, window, alpha, cpu_iters):
+def cpu_baseline(rows, cols, window, alpha, cpu_iters, threads=1):
     """oracle/ float64 port of hornSchunck.cpp (pass-per-OpenCV-call, fresh
-    temporaries each iteration), 1 thread, on the same synthetic pair at full
-    size for a bounded number of iterations."""
+    temporaries each iteration) on the same synthetic pair at full size for a
+    bounded number of iterations; 1 thread like the reference,
+    or `threads` OpenMP threads for the all-cores variant."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     import hsflow
     I0, I1 = hsflow.synth_pair(1000, rows, cols)
     if not cpu_iters:
         t = time.perf_counter()
-        oracle.flow(I0, I1, window, 1, alpha, nthreads=1)
+        oracle.flow(I0, I1, window, 1, alpha, nthreads=threads)
         one = time.perf_counter() - t
         cpu_iters = max(1, min(60, int(15.0 / max(one, 1e-3))))
     t = time.perf_counter()
-    oracle.flow(I0, I1, window, cpu_iters, alpha, nthreads=1)
+    oracle.flow(I0, I1, window, cpu_iters, alpha, nthreads=threads)
     dt = time.perf_counter() - t
     return {"value": round(rows * cols * cpu_iters / dt / 1e6, 2), "unit": "Mpix*iter/s",
-            "cores": 1, "kind": "port",
+            "cores": threads, "kind": "port",
             "sample": f"{cols}x{rows} pair, {cpu_iters} Jacobi iterations incl. gradients, "
                       f"float64, {dt:.1f} s"}
 
