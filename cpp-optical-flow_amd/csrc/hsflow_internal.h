@@ -19,9 +19,7 @@ struct JacobiArgs {
     const uint32_t *flags;     // per pair: 0 -> gpack valid, else f32 planes
     int ablate;                // diagnostics only (HSFLOW_ABLATE): 1 = no
                                // iterations (memory only), 2 = no memory
-                               // traffic (descriptors of size 0), 3 = no
-                               // slab barrier, 4 = 3 + own-slab LDS reads
-                               // (3/4 give wrong results: timing only)
+                               // traffic (descriptors of size 0)
 };
 
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,

@@ -392,40 +392,104 @@ __global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
 //    which depends only on the column's parity within the region (region
 //    origins are even for every KB), so every KB gives identical bits.
 
-// Horizontal window sums of two columns per lane (e = even, o = odd column)
-// for two fields at once, statements interleaved for the DPP wait states.
+// Horizontal window sums of two columns per lane (e = even, o = odd column),
+// any window 2..9.  The window of column c is [c - A, c + AR].  Lane offset j
+// contributes P = e + o, e alone, o alone or nothing; the sum is evaluated
+// from both ends inwards, one fused DPP add per lane spanned:
+//   accL = c(-m); accL = L(accL) + c(j) for j = -m+1..-1   (L: lane l <- l-1)
+//   accR = c(+m'); accR = R(accR) + c(j) for j = m'-1..1    (R: lane l <- l+1)
+//   sum  = (L(accL) + c(0)) + R(accR)
+// For w = 5 this is ((P(l-1) + P(l)) + e(l+1)) and ((o(l-1) + P(l)) + P(l+1)),
+// for w = 3 (o(l-1) + P(l)) and (P(l) + e(l+1)).  The association depends only
+// on the column's parity, so every blocking depth gives identical bits.
+template <int A, int AR>
+struct HWin {
+    // contribution of lane offset j to the window of an even (odd = 0) or odd
+    // column: 0 none, 1 e, 2 o, 3 P
+    static constexpr int kind(int j, int odd) {
+        const int ce = 2 * j - odd, co = 2 * j + 1 - odd;  // offsets of e, o
+        const bool ie = ce >= -A && ce <= AR, io = co >= -A && co <= AR;
+        return (ie ? 1 : 0) | (io ? 2 : 0);
+    }
+    static constexpr int left(int odd) {  // lanes spanned to the left
+        int m = 0;
+        while (kind(-(m + 1), odd) != 0) ++m;
+        return m;
+    }
+    static constexpr int right(int odd) {
+        int m = 0;
+        while (kind(m + 1, odd) != 0) ++m;
+        return m;
+    }
+};
+
+template <int A, int AR, int ODD>
+__device__ __forceinline__ float hwin(float e, float o, float P) {
+    using H = HWin<A, AR>;
+    constexpr int mL = H::left(ODD), mR = H::right(ODD);
+    auto c = [&](int j) {
+        const int k = H::kind(j, ODD);
+        return k == 3 ? P : (k == 1 ? e : o);
+    };
+    float s = c(0);
+    if constexpr (mL > 0) {
+        float acc = c(-mL);
+#pragma unroll
+        for (int j = -mL + 1; j <= -1; ++j) acc = from_left(acc) + c(j);
+        s = from_left(acc) + s;
+    }
+    if constexpr (mR > 0) {
+        float acc = c(mR);
+#pragma unroll
+        for (int j = mR - 1; j >= 1; --j) acc = from_right(acc) + c(j);
+        s = s + from_right(acc);
+    }
+    return launder_f(s);
+}
+
+// both columns of both fields; statements of u and v interleave after
+// scheduling, so each DPP read of a just-written VGPR has independent work
+// as its wait state
 template <int W>
 __device__ __forceinline__ void hsum_c2(float ue, float uo, float ve, float vo, float &hue,
                                         float &huo, float &hve, float &hvo) {
+    constexpr int A = W - W / 2 - 1, AR = W / 2;
     const float pu = ue + uo;
     const float pv = ve + vo;
     if constexpr (W == 5) {
-        // even 2l:   (x-2 + x-1) + (x + x+1) + x+2  = (P(l-1) + P(l)) + e(l+1)
-        // odd 2l+1:  (x-1 + (x + x+1)) + (x+2 + x+3) = (o(l-1) + P(l)) + P(l+1)
+        // the same sums as hwin, hand-interleaved (this order keeps the
+        // 10-row w = 5 kernel within 128 VGPRs without spills)
         const float au = from_left(pu) + pu;
         const float av = from_left(pv) + pv;
         const float bu = from_left(uo) + pu;
         const float bv = from_left(vo) + pv;
-        // launder pins each sum to its row: otherwise IR sinking moves the
-        // adds (and keeps the unfused DPP copies live) to the rows that use them
         hue = launder_f(au + from_right(ue));
         hve = launder_f(av + from_right(ve));
         huo = launder_f(bu + from_right(pu));
         hvo = launder_f(bv + from_right(pv));
-    } else {
-        static_assert(W == 3, "hsum_c2: windows 3 and 5");
-        // even 2l: x-1 + (x + x+1);  odd 2l+1: (x-1 + x) + x+1
+    } else if constexpr (W == 3) {
         hue = launder_f(from_left(uo) + pu);
         hve = launder_f(from_left(vo) + pv);
         huo = launder_f(pu + from_right(ue));
         hvo = launder_f(pv + from_right(ve));
+    } else {
+        hue = hwin<A, AR, 0>(ue, uo, pu);
+        hve = hwin<A, AR, 0>(ve, vo, pv);
+        huo = hwin<A, AR, 1>(ue, uo, pu);
+        hvo = hwin<A, AR, 1>(ve, vo, pv);
     }
 }
 
+// workgroup-kernel geometry per window: slab rows per wave (deeper register
+// rings for wider windows) and double-buffered slab exchange while two
+// workgroups' W-1 boundary rows fit in LDS
+constexpr int wg_rows(int W) { return W <= 5 ? 10 : (W <= 7 ? 8 : 7); }
+constexpr bool wg_double_buffer(int W) { return W <= 5; }
+
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
-                                        float2 (&xch)[2][NW][W - 1][2][64], int tx,
-                                        int ty, int wv, int lane, size_t pbase,
+                                        float2 (&xch)[wg_double_buffer(W) ? 2 : 1][NW][W - 1][2][64],
+                                        int tx, int ty, int wv, int lane, size_t pbase,
                                         int plane_bytes);
 
 // 4 waves per SIMD (<= 128 VGPRs): two 8-wave workgroups per CU
@@ -442,7 +506,7 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     static_assert(OX > 0 && OY > 0 && (OX % 2) == 0, "geometry");
     static_assert(RW <= 64, "row mask is 64 bits");
     // [parity][wave][boundary row][field u/v][lane] of (even, odd) columns
-    __shared__ float2 xch[2][NW][NB][2][64];
+    __shared__ float2 xch[wg_double_buffer(W) ? 2 : 1][NW][NB][2][64];
 
     // XCD-aware workgroup order (see hs_jacobi_kernel)
     const int nblk = gridDim.x * gridDim.y;
@@ -495,8 +559,8 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
 
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
-                                        float2 (&xch)[2][NW][W - 1][2][64], int tx,
-                                        int ty, int wv, int lane, size_t pbase,
+                                        float2 (&xch)[wg_double_buffer(W) ? 2 : 1][NW][W - 1][2][64],
+                                        int tx, int ty, int wv, int lane, size_t pbase,
                                         int plane_bytes) {
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
     constexpr int HL = KB * A, HR = KB * AR;
@@ -610,12 +674,12 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
 
     const int n_it = p.ablate == 1 ? 0 : p.iters;
     for (int it = 0; it < n_it; ++it) {
-        const int par = it & 1;
+        const int par = wg_double_buffer(W) ? (it & 1) : 0;
         // 1. horizontal sums of the boundary rows first, published for the
         //    neighbouring slabs: rows 0..AR-1 feed the wave above, rows
         //    RW-A..RW-1 the wave below.  Exchanging sums (not raw rows)
         //    means no wave recomputes another slab's rows.
-        f2v htu[AR], htv[AR], hbu[A], hbv[A];
+        f2v htu[AR > 0 ? AR : 1], htv[AR > 0 ? AR : 1], hbu[A > 0 ? A : 1], hbv[A > 0 ? A : 1];
 #pragma unroll
         for (int k = 0; k < AR; ++k) {
             hrow(k, htu[k], htv[k]);
@@ -628,7 +692,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
             xch[par][wv][AR + k][0][lane] = make_float2(hbu[k].x, hbu[k].y);
             xch[par][wv][AR + k][1][lane] = make_float2(hbv[k].x, hbv[k].y);
         }
-        if (p.ablate < 3) __syncthreads();  // 3/4: timing diagnostics only
+        __syncthreads();
 
         // 2. sweep slab rows t = -A .. RW+AR-1 through a ring of horizontal
         //    sums (hu, hv) and vertical pair sums q(t) = h(t) + h(t+1)
@@ -638,8 +702,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
         // the HL (HR) halo rows, which are never stored; at the image border
         // those rows are re-zeroed every iteration (EDGE).  So the reads are
         // unconditional, from a clamped slab (no branches, no zero fill).
-        const int wa = p.ablate == 4 ? wv : (wv > 0 ? wv - 1 : 0);
-        const int wb = p.ablate == 4 ? wv : (wv < NW - 1 ? wv + 1 : NW - 1);
+        const int wa = wv > 0 ? wv - 1 : 0, wb = wv < NW - 1 ? wv + 1 : NW - 1;
         f2v hu[W], hv[W], qu[W], qv[W];
 #pragma unroll
         for (int rr = 0; rr < RW + NB; ++rr) {
@@ -671,18 +734,29 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
             }
             const int y = t - AR;  // slab row whose window ends at t
             if (y >= 0) {
+                // pair tree over rows y-A .. y+AR:
+                // ((q(y-A) + q(y-A+2)) + ...) [+ h(y+AR) for odd W], e.g.
+                // w = 5: (q(y-2) + q(y)) + h(y+2);  w = 3: q(y-1) + h(y+1)
                 f2v su, sv;
-                if constexpr (W == 5) {
-                    // (h(y-2) + h(y-1)) + (h(y) + h(y+1)) + h(y+2)
+                if constexpr (W == 5) {  // the tree below, written out
                     const int s0 = (y - 2 + 2 * W) % W, s1 = (y + 2 * W) % W,
                               s2 = (y + 2 + 2 * W) % W;
                     su = (qu[s0] + qu[s1]) + hu[s2];
                     sv = (qv[s0] + qv[s1]) + hv[s2];
                 } else {
-                    // (h(y-1) + h(y)) + h(y+1)
-                    const int s0 = (y - 1 + 2 * W) % W, s2 = (y + 1 + 2 * W) % W;
-                    su = qu[s0] + hu[s2];
-                    sv = qv[s0] + hv[s2];
+                    su = qu[(y - A + 2 * W) % W];
+                    sv = qv[(y - A + 2 * W) % W];
+#pragma unroll
+                    for (int pq = 1; pq < W / 2; ++pq) {
+                        const int sq = (y - A + 2 * pq + 2 * W) % W;
+                        su = su + qu[sq];
+                        sv = sv + qv[sq];
+                    }
+                    if constexpr (W & 1) {
+                        const int sh = (y + AR + 2 * W) % W;
+                        su = su + hu[sh];
+                        sv = sv + hv[sh];
+                    }
                 }
                 const f2v ub = su * invv, vb = sv * invv;
                 const f2v xv = X[y], yv = Y[y];
@@ -703,6 +777,9 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
             }
             if ((rr % SB) == SB - 1) __builtin_amdgcn_sched_barrier(0);
         }
+        // single-buffered exchange: the neighbours' reads of this iteration
+        // must finish before the next iteration's publish overwrites them
+        if constexpr (!wg_double_buffer(W)) __syncthreads();
     }
 
     // interior tile: workgroup rows [HL, HL + OY), lanes [HLc/2, (HLc + OX)/2)
@@ -817,7 +894,9 @@ static int k2_variant() {
     return v;
 }
 
-static bool uses_wg_kernel(int W) { return (W == 3 || W == 5) && k2_variant() != 0; }
+// windows 3..9; w = 1, 2 keep the per-wave kernel (a 1-column halo makes
+// it fast already: 920 k Mpix*iter/s at w = 2), wider windows the generic one
+static bool uses_wg_kernel(int W) { return W >= 3 && W <= 9 && k2_variant() != 0; }
 
 // Temporal-blocking depth per window (overridable through
 // hsflow_set_iters_per_launch).  The workgroup kernel (W = 3, 5) takes
@@ -828,7 +907,17 @@ int default_kb(int W) {
     // measured on MI355X (scripts/sweep.py, profiles/README.md): the extra
     // halo work of deeper blocking is cheaper than the HBM pass it saves up
     // to KB(W-1) = 24 for W = 5 and 16 for W = 3 (10/12/16 measured, no gain)
-    if (uses_wg_kernel(W)) return W == 3 ? 8 : 6;
+    if (uses_wg_kernel(W)) {
+        // about 24 halo rows per launch (measured optimum at w = 5: KB 6)
+        switch (W) {
+        case 3: return 8;
+        case 4: return 8;
+        case 5: return 6;
+        case 6: return 5;
+        case 7: return 4;
+        default: return 3;  // 8, 9
+        }
+    }
     if (W < 1 || W > 9) return 1;
     for (int kb : {8, 4, 2})
         if (kb_ok_f32(W, kb)) return kb;
@@ -866,6 +955,11 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
 
 template <int W, int KB>
 static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
+    if constexpr (KB * (W - 1) > 32) {  // kb_supported() rejects these
+        (void)a;
+        (void)s;
+        return hipErrorInvalidValue;
+    } else {
     // 8 waves x 10 slab rows (80 x 128 region, 128 VGPRs, no spills).
     // Same-box A/B on MI355X (scripts/ab_bench.sh), W = 5, KB = 6:
     // 8 rows 820k / 941k, 9 rows 850k / 995k, 10 rows 863k / 1026k
@@ -874,12 +968,13 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     // per CU).  SB = 16 > rows swept: no scheduling barriers inside the
     // sweep, so the scheduler interleaves rows and fills the DPP
     // read-after-write wait states.
-    return launch_jacobi_wg<W, KB, 10, 8, 16>(a, s);
+    return launch_jacobi_wg<W, KB, wg_rows(W), 8, 16>(a, s);
+    }
 }
 
 template <int W>
 static hipError_t launch_jacobi_w(JacobiArgs a, int KB, hipStream_t s) {
-    if constexpr (W == 3 || W == 5) {
+    if constexpr (W >= 3 && W <= 9) {
         if (k2_variant() != 0) {
             switch (KB) {
             case 1: return launch_jacobi_wgv<W, 1>(a, s);

@@ -188,6 +188,29 @@ def test_blocking_depth_is_bit_invariant(hs, dtype, cols):
         assert np.array_equal(got[0], ref3[0]), kb
 
 
+@pytest.mark.parametrize("w", [4, 6, 7, 8, 9])
+@pytest.mark.parametrize("cols", [301, 302])
+@pytest.mark.parametrize("integral", [True, False])
+def test_blocking_depth_bit_invariant_wide_windows(hs, w, cols, integral):
+    """Windows 3..9 share the workgroup kernel (generic horizontal/vertical
+    trees): every supported blocking depth gives the same bits, and the
+    result matches the float64 oracle."""
+    import torch
+    I0, I1 = hs.synth_pair(77, 190, cols)
+    if not integral:
+        I0 = I0 * np.float32(0.9) + np.float32(0.35)
+    t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
+    n = 13
+    ref = _device_flow(hs, t0, t1, w, n, 1)
+    for kb in (2, 3, 4, 5, 6, 8):
+        if kb * (w - 1) > 32:
+            continue
+        got = _device_flow(hs, t0, t1, w, n, kb)
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), kb
+    uo, vo = oracle.flow(I0, I1, w, n, 1.0, nthreads=8)
+    assert norm_rel_err(ref[0], uo) <= TOL and norm_rel_err(ref[1], vo) <= TOL
+
+
 @pytest.mark.parametrize("cols", [333, 334])
 def test_blocking_depth_bit_invariant_f32_gradients(hs, cols):
     import torch
