@@ -354,3 +354,37 @@ def test_cpp_main_driver_reproduces_reference_plot(tmp_path, tag):
     b = read_pgm(os.path.join(GOLDEN, f"kitti_{tag}_11.pgm"))
     uo, _ = _oracle_flow(a, b, 5, 100)
     assert norm_rel_err(u, uo) <= TOL
+
+
+@pytest.mark.parametrize("batch", [1, 3])
+def test_device_solve_captures_into_a_hip_graph(hs, batch):
+    """include/hsflow.h: the *_device calls are stream-ordered and never
+    allocate or synchronise, so a whole solve (K1, the K2 passes, the batch
+    split over side streams with event fork/join) can be captured into a
+    hipGraph and replayed; the replay gives the eager result bit for bit."""
+    import torch
+    pairs = [hs.synth_pair(1500 + k, 120, 210) for k in range(batch)]
+    t0 = torch.stack([torch.from_numpy(p[0]) for p in pairs]).cuda()
+    t1 = torch.stack([torch.from_numpy(p[1]) for p in pairs]).cuda()
+    u = torch.empty_like(t0)
+    v = torch.empty_like(t0)
+    ws = hs.alloc_workspace(120, 210, batch)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        hs.flow_device(t0, t1, 5, 40, 1.0, u, v, ws)   # eager (creates side streams)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    ref = (u.clone(), v.clone())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        hs.flow_device(t0, t1, 5, 40, 1.0, u, v, ws)
+    u.zero_()
+    v.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(u, ref[0]) and torch.equal(v, ref[1])
+    t0.add_(0)  # inputs unchanged; a second replay is identical too
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(u, ref[0])
