@@ -131,10 +131,13 @@ int pick_kb(int window, bool need_f32) {
 }
 
 // Per-thread, per-device side streams for splitting a batch: each sub-batch
-// runs its Jacobi passes on its own stream, so the load/compute phases of
-// concurrent K2 launches overlap (measured +8..19 % at 8 x 1080p).  Fork and
-// join are event based (capturable into a hipGraph).  Never destroyed: they
-// live until the process exits (no static-destruction-order hazards).
+// runs its Jacobi passes on its own stream, so the launches of the two halves
+// overlap (one's tail and boundary with the other's work).  Default 2 halves:
+// same-box bench, 1080p x 8 / 4K x 2 Mpix*iter/s: 1 stream 905k / 960k,
+// 2 streams 967k / 1034k, 4 streams 901k / 1033k, 8 streams 865k / 1032k
+// (scripts/streams_ab.sh).  Fork and join are event based (capturable into a
+// hipGraph).  Never destroyed: they live until the process exits (no
+// static-destruction-order hazards).
 struct SidePool {
     int device = -1;
     std::vector<hipStream_t> streams;
@@ -146,7 +149,7 @@ int g_split_override = 0;
 int max_split() {
     static const int n = [] {
         const char *e = getenv("HSFLOW_STREAMS");
-        int k = e ? atoi(e) : 8;
+        int k = e ? atoi(e) : 2;
         return k < 1 ? 1 : (k > 16 ? 16 : k);
     }();
     return g_split_override > 0 ? g_split_override : n;

@@ -121,8 +121,8 @@ int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
 
 /* Batches of >= 2 pairs are split over up to n side streams (forked from and
  * joined back to the caller's stream with events) so that concurrent Jacobi
- * launches overlap their load and compute phases.  1 disables; 0 restores
- * the default (8, or HSFLOW_STREAMS).  Process-wide. */
+ * launches overlap.  1 disables; 0 restores the default (2, or
+ * HSFLOW_STREAMS).  Process-wide. */
 int hsflow_set_max_streams(int n);
 
 /* ---- coarse-to-fine warm start (north_star config 5) ---------------------
