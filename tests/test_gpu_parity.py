@@ -291,6 +291,33 @@ def test_1080p_against_oracle(hs):
     assert 0.05 < float(u.mean()) < 0.3
 
 
+def test_config2_full_length_against_oracle(hs):
+    """BASELINE configs[1] exactly: 1920x1080 f32 synthetic pair, alpha 1,
+    300 iterations, w 5 -- GPU vs the float64 oracle at full length
+    (oracle on 16 threads, ~15 s)."""
+    import torch
+    I0, I1 = hs.synth_pair(1000, 1080, 1920)
+    u, v = hs.flow_device(torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda(),
+                          5, 300, 1.0)
+    uo, vo = oracle.flow(I0, I1, 5, 300, 1.0, nthreads=16)
+    assert norm_rel_err(u.cpu().numpy(), uo) <= TOL
+    assert norm_rel_err(v.cpu().numpy(), vo) <= TOL
+
+
+def test_config3_full_length_against_oracle(hs):
+    """BASELINE configs[2] exactly: 3840x2160 f32 synthetic pair, 500
+    iterations, w 5 -- GPU vs the float64 oracle at full size and length
+    (oracle on 16 threads, ~70 s)."""
+    import torch
+    I0, I1 = hs.synth_pair(1000, 2160, 3840)
+    u, v = hs.flow_device(torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda(),
+                          5, 500, 1.0)
+    uo, vo = oracle.flow(I0, I1, 5, 500, 1.0, nthreads=16)
+    eu, ev = norm_rel_err(u.cpu().numpy(), uo), norm_rel_err(v.cpu().numpy(), vo)
+    print(f"config 3 full length: max|du|/max|u| = {eu:.2e}, dv {ev:.2e}")
+    assert eu <= TOL and ev <= TOL
+
+
 def test_4k_500_properties(hs):
     """Config 3 shape at full iteration count: size-independent properties
     (KB invariance, batch==single, finite, expected mean motion)."""
