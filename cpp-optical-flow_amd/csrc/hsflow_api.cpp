@@ -72,9 +72,14 @@ size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 // Largest frame: plane bytes must fit the 31-bit buffer offsets of K2.
 constexpr long long kMaxPlanePixels = (1ll << 29) - 1;
 
+// Largest batch: pairs index gridDim.y / gridDim.z of the kernels (65535);
+// tallest plane: the 64 x 4 per-pixel kernels put rows / 4 in gridDim.y.
+constexpr int kMaxBatch = 65535;
+constexpr int kMaxRows = 4 * 65535;
+
 bool sizes_ok(int rows, int cols, int batch) {
-    return rows >= 1 && cols >= 1 && batch >= 1 &&
-           (long long)rows * cols <= kMaxPlanePixels;
+    return rows >= 1 && rows <= kMaxRows && cols >= 1 && batch >= 1 &&
+           batch <= kMaxBatch && (long long)rows * cols <= kMaxPlanePixels;
 }
 
 struct Workspace {

@@ -25,29 +25,31 @@ __device__ __forceinline__ uint32_t gray1(uint32_t B, uint32_t G, uint32_t R) {
     return (9798u * R + 19235u * G + 3735u * B + 16384u) >> 15;
 }
 
-// grid (ceil(cols/4 / 64), rows, batch), block 64
+// grid (ceil(cols/4 / 64), min(rows, 65535), batch), block 64; rows beyond
+// gridDim.y are visited grid-stride
 __global__ __launch_bounds__(64) void hs_bgr2gray_kernel(const uint8_t *__restrict__ bgr,
                                                          int rows, int cols,
                                                          uint8_t *__restrict__ gray) {
     const int x4 = (blockIdx.x * 64 + threadIdx.x) * 4;
-    const int y = blockIdx.y;
     if (x4 >= cols) return;
     const size_t plane = (size_t)rows * cols;
-    const uint8_t *src = bgr + (blockIdx.z * plane + (size_t)y * cols) * 3;
-    uint8_t *dst = gray + blockIdx.z * plane + (size_t)y * cols;
-    if ((cols & 3) == 0) {
-        const uint32_t *s = (const uint32_t *)(src + (size_t)x4 * 3);
-        const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
-        // bytes: B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3
-        const uint32_t g0 = gray1(w0 & 0xFF, (w0 >> 8) & 0xFF, (w0 >> 16) & 0xFF);
-        const uint32_t g1 = gray1(w0 >> 24, w1 & 0xFF, (w1 >> 8) & 0xFF);
-        const uint32_t g2 = gray1((w1 >> 16) & 0xFF, w1 >> 24, w2 & 0xFF);
-        const uint32_t g3 = gray1((w2 >> 8) & 0xFF, (w2 >> 16) & 0xFF, w2 >> 24);
-        *(uint32_t *)(dst + x4) = g0 | (g1 << 8) | (g2 << 16) | (g3 << 24);
-    } else {
-        for (int k = 0; k < 4 && x4 + k < cols; ++k) {
-            const uint8_t *p = src + (size_t)(x4 + k) * 3;
-            dst[x4 + k] = (uint8_t)gray1(p[0], p[1], p[2]);
+    for (int y = blockIdx.y; y < rows; y += gridDim.y) {
+        const uint8_t *src = bgr + (blockIdx.z * plane + (size_t)y * cols) * 3;
+        uint8_t *dst = gray + blockIdx.z * plane + (size_t)y * cols;
+        if ((cols & 3) == 0) {
+            const uint32_t *s = (const uint32_t *)(src + (size_t)x4 * 3);
+            const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
+            // bytes: B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3
+            const uint32_t g0 = gray1(w0 & 0xFF, (w0 >> 8) & 0xFF, (w0 >> 16) & 0xFF);
+            const uint32_t g1 = gray1(w0 >> 24, w1 & 0xFF, (w1 >> 8) & 0xFF);
+            const uint32_t g2 = gray1((w1 >> 16) & 0xFF, w1 >> 24, w2 & 0xFF);
+            const uint32_t g3 = gray1((w2 >> 8) & 0xFF, (w2 >> 16) & 0xFF, w2 >> 24);
+            *(uint32_t *)(dst + x4) = g0 | (g1 << 8) | (g2 << 16) | (g3 << 24);
+        } else {
+            for (int k = 0; k < 4 && x4 + k < cols; ++k) {
+                const uint8_t *p = src + (size_t)(x4 + k) * 3;
+                dst[x4 + k] = (uint8_t)gray1(p[0], p[1], p[2]);
+            }
         }
     }
 }
@@ -57,7 +59,7 @@ __global__ __launch_bounds__(64) void hs_bgr2gray_kernel(const uint8_t *__restri
 hipError_t launch_bgr2gray(const uint8_t *bgr, int rows, int cols, int batch,
                            uint8_t *gray, hipStream_t s) {
     const int quads = (cols + 3) / 4;
-    dim3 grd((quads + 63) / 64, rows, batch);
+    dim3 grd((quads + 63) / 64, rows < 65535 ? rows : 65535, batch);
     hipLaunchKernelGGL(hs_bgr2gray_kernel, grd, dim3(64), 0, s, bgr, rows, cols, gray);
     return hipGetLastError();
 }

@@ -89,7 +89,7 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
                      void *gt, int dtype_out, size_t out_step);
 
 /* ---- device pointers, stream-ordered ------------------------------------
- * A batch is `batch` independent frame pairs stored back to back:
+ * A batch is `batch` (1..65535) independent frame pairs stored back to back:
  * I0[b][rows][cols], dense (pitch = cols elements), likewise u, v.
  * Inputs are U8, F16 or F32.  Outputs are f32.  `stream` is a hipStream_t (NULL =
  * default stream).  `workspace` is device memory of at least

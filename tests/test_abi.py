@@ -117,3 +117,12 @@ def test_header_is_plain_c_and_links_from_c(tmp_path):
     # OpenCV 4.x 15-bit BGR2GRAY of (B,G,R) = (10,20,30) and (200,100,0)
     assert (g0, g1) == ((9798 * 30 + 19235 * 20 + 3735 * 10 + 16384) >> 15,
                         (9798 * 0 + 19235 * 100 + 3735 * 200 + 16384) >> 15)
+
+
+def test_batch_and_plane_limits_are_rejected_on_the_host():
+    assert hsflow.workspace_bytes(10, 10, 65535) > 0
+    assert hsflow.workspace_bytes(10, 10, 65536) == 0          # gridDim limit
+    assert hsflow.workspace_bytes(1 << 14, (1 << 15) - 1, 1) > 0   # < 2^29 px: accepted
+    assert hsflow.workspace_bytes(1 << 14, 1 << 15, 1) == 0        # 2^29 px: offsets overflow
+    assert hsflow.workspace_bytes(4 * 65535, 8, 1) > 0             # tallest plane
+    assert hsflow.workspace_bytes(4 * 65535 + 1, 8, 1) == 0        # gridDim.y of K1

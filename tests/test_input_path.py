@@ -38,7 +38,8 @@ def test_device_gray_matches_fixture(hs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(1, 1), (3, 5), (7, 37), (64, 128), (33, 1001)])
+@pytest.mark.parametrize("shape", [(1, 1), (3, 5), (7, 37), (64, 128), (33, 1001),
+                                   (70001, 9), (65536, 8)])
 def test_device_gray_matches_host_and_oracle(hs, shape):
     import torch
     bgr = _bgr(*shape)
