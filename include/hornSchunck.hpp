@@ -32,7 +32,8 @@ class hornSchunck {
 
     void getGradients(cv::Mat imagePrev, cv::Mat imageNext, cv::Mat &gradX, cv::Mat &gradY,
                       cv::Mat &gradT) {
-        const hsflow::ImageView a = as_view(imagePrev), b = as_view(imageNext);
+        cv::Mat ha, hb;  // converted copies for depths the ABI does not take
+        const hsflow::ImageView a = as_view(imagePrev, ha), b = as_view(imageNext, hb);
         gradX.create(imagePrev.rows, imagePrev.cols, CV_64FC1);
         gradY.create(imagePrev.rows, imagePrev.cols, CV_64FC1);
         gradT.create(imagePrev.rows, imagePrev.cols, CV_64FC1);
@@ -48,7 +49,8 @@ class hornSchunck {
 
     void getFlow(cv::Mat imagePrev, cv::Mat imageNext, cv::Mat &u, cv::Mat &v) {
         sync_params();
-        const hsflow::ImageView a = as_view(imagePrev), b = as_view(imageNext);
+        cv::Mat ha, hb;
+        const hsflow::ImageView a = as_view(imagePrev, ha), b = as_view(imageNext, hb);
         // hornSchunck.cpp:49-50: u, v are (re)allocated as CV_64FC1
         u.create(imagePrev.rows, imagePrev.cols, CV_64FC1);
         v.create(imagePrev.rows, imagePrev.cols, CV_64FC1);
@@ -68,26 +70,32 @@ class hornSchunck {
         impl_.maxIterations = maxIterations;
         impl_.alpha = alpha;
     }
-    static hsflow::ImageView as_view(const cv::Mat &m) {
+    // A view of m for the C ABI; depths the ABI does not take are converted
+    // into `holder` first, exactly as hornSchunck.cpp:23-24 converts every
+    // input with convertTo(CV_64FC1).
+    static hsflow::ImageView as_view(const cv::Mat &m, cv::Mat &holder) {
         if (m.empty()) CV_Error(cv::Error::StsBadArg, "empty image");
         if (m.channels() != 1)
             CV_Error(cv::Error::StsBadArg, "hornSchunck expects single-channel images "
                                            "(main.cpp:11-26 converts BGR to gray first)");
-        hsflow::ImageView v;
-        v.data = m.data;
-        v.rows = m.rows;
-        v.cols = m.cols;
-        v.step = m.step;
+        const cv::Mat *src = &m;
+        int type;
         switch (m.depth()) {
-        case CV_8U: v.type = HSFLOW_U8; break;
-        case CV_32F: v.type = HSFLOW_F32; break;
-        case CV_64F: v.type = HSFLOW_F64; break;
-        default: {
-            // other depths: convertTo(CV_64FC1) exactly as hornSchunck.cpp:23-24
-            CV_Error(cv::Error::StsUnsupportedFormat,
-                     "convert the frame to CV_8U, CV_32F or CV_64F first");
+        case CV_8U: type = HSFLOW_U8; break;
+        case CV_16F: type = HSFLOW_F16; break;
+        case CV_32F: type = HSFLOW_F32; break;
+        case CV_64F: type = HSFLOW_F64; break;
+        default:  // CV_8S, CV_16U, CV_16S, CV_32S
+            m.convertTo(holder, CV_64FC1);
+            src = &holder;
+            type = HSFLOW_F64;
         }
-        }
+        hsflow::ImageView v;
+        v.data = src->data;
+        v.rows = src->rows;
+        v.cols = src->cols;
+        v.step = src->step;
+        v.type = type;
         return v;
     }
 };
