@@ -33,22 +33,10 @@
 #include <stdlib.h>
 
 #include "hsflow_internal.h"
+#include "hsflow_device.h"
 
 namespace hsflow {
 
-// ------------------------------------------------------------------ packing
-__device__ __forceinline__ uint32_t pack_grad(int ix, int iy, int it) {
-    return ((uint32_t)ix & 0x7FFu) | (((uint32_t)iy & 0x7FFu) << 11) |
-           (((uint32_t)it & 0x1FFu) << 22);
-}
-__device__ __forceinline__ void unpack_grad(uint32_t p, float &ix, float &iy,
-                                            float &it) {
-    // v_bfe_i32 sign-extends; the builtin is typed unsigned, so cast back to
-    // int before converting (else v_cvt_f32_u32 turns -1 into 4.29e9)
-    ix = (float)(int)__builtin_amdgcn_sbfe(p, 0, 11);
-    iy = (float)(int)__builtin_amdgcn_sbfe(p, 11, 11);
-    it = (float)(int)__builtin_amdgcn_sbfe(p, 22, 9);
-}
 
 __device__ __forceinline__ int reflect101(int p, int len) {
     // OpenCV borderInterpolate(BORDER_REFLECT_101) for |overshoot| <= 1.
@@ -100,17 +88,6 @@ __global__ __launch_bounds__(256) void hs_gradients_kernel(
 }
 
 // ----------------------------------------------------------------------- K2
-// Cross-lane shifts by one lane over the whole wavefront: DPP wave_shr:1 /
-// wave_shl:1 (GFX9-family DPP, kept on gfx950).  They fuse into the consuming
-// v_add_f32 as a DPP source modifier: pure VALU, no LDS crossbar traffic.
-// Lanes shifted in from outside the wave read 0 (bound_ctrl); those results
-// only ever land in the region's halo columns, which are never stored.
-__device__ __forceinline__ float from_left(float x) {  // lane l <- lane l-1
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x138, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float from_right(float x) {  // lane l <- lane l+1
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x130, 0xF, 0xF, true));
-}
 
 // Horizontal window sum over lanes [l - A, l + W-1-A] (A = anchor).  The
 // summation order is fixed per W, so every blocking depth gives the same bits.
@@ -167,26 +144,6 @@ template <int W> __device__ __forceinline__ float hsum(float x) {
     }
 }
 
-// Keep the compiler from CSE-ing an address computation across the
-// iteration loop (that would pin RH extra VGPRs for the whole solve).
-__device__ __forceinline__ int launder(int x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2v launder_v2(f2v x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ uint32_t launder_u(uint32_t x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ float launder_f(float x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
 
 // One wavefront's work on one region: rows [r0, r0 + RH) x the 64 columns
 // starting at gc - lane; KB iterations; writes region rows [HL, HL + nout)
@@ -392,93 +349,6 @@ __global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
 //    which depends only on the column's parity within the region (region
 //    origins are even for every KB), so every KB gives identical bits.
 
-// Horizontal window sums of two columns per lane (e = even, o = odd column),
-// any window 2..9.  The window of column c is [c - A, c + AR].  Lane offset j
-// contributes P = e + o, e alone, o alone or nothing; the sum is evaluated
-// from both ends inwards, one fused DPP add per lane spanned:
-//   accL = c(-m); accL = L(accL) + c(j) for j = -m+1..-1   (L: lane l <- l-1)
-//   accR = c(+m'); accR = R(accR) + c(j) for j = m'-1..1    (R: lane l <- l+1)
-//   sum  = (L(accL) + c(0)) + R(accR)
-// For w = 5 this is ((P(l-1) + P(l)) + e(l+1)) and ((o(l-1) + P(l)) + P(l+1)),
-// for w = 3 (o(l-1) + P(l)) and (P(l) + e(l+1)).  The association depends only
-// on the column's parity, so every blocking depth gives identical bits.
-template <int A, int AR>
-struct HWin {
-    // contribution of lane offset j to the window of an even (odd = 0) or odd
-    // column: 0 none, 1 e, 2 o, 3 P
-    static constexpr int kind(int j, int odd) {
-        const int ce = 2 * j - odd, co = 2 * j + 1 - odd;  // offsets of e, o
-        const bool ie = ce >= -A && ce <= AR, io = co >= -A && co <= AR;
-        return (ie ? 1 : 0) | (io ? 2 : 0);
-    }
-    static constexpr int left(int odd) {  // lanes spanned to the left
-        int m = 0;
-        while (kind(-(m + 1), odd) != 0) ++m;
-        return m;
-    }
-    static constexpr int right(int odd) {
-        int m = 0;
-        while (kind(m + 1, odd) != 0) ++m;
-        return m;
-    }
-};
-
-template <int A, int AR, int ODD>
-__device__ __forceinline__ float hwin(float e, float o, float P) {
-    using H = HWin<A, AR>;
-    constexpr int mL = H::left(ODD), mR = H::right(ODD);
-    auto c = [&](int j) {
-        const int k = H::kind(j, ODD);
-        return k == 3 ? P : (k == 1 ? e : o);
-    };
-    float s = c(0);
-    if constexpr (mL > 0) {
-        float acc = c(-mL);
-#pragma unroll
-        for (int j = -mL + 1; j <= -1; ++j) acc = from_left(acc) + c(j);
-        s = from_left(acc) + s;
-    }
-    if constexpr (mR > 0) {
-        float acc = c(mR);
-#pragma unroll
-        for (int j = mR - 1; j >= 1; --j) acc = from_right(acc) + c(j);
-        s = s + from_right(acc);
-    }
-    return launder_f(s);
-}
-
-// both columns of both fields; statements of u and v interleave after
-// scheduling, so each DPP read of a just-written VGPR has independent work
-// as its wait state
-template <int W>
-__device__ __forceinline__ void hsum_c2(float ue, float uo, float ve, float vo, float &hue,
-                                        float &huo, float &hve, float &hvo) {
-    constexpr int A = W - W / 2 - 1, AR = W / 2;
-    const float pu = ue + uo;
-    const float pv = ve + vo;
-    if constexpr (W == 5) {
-        // the same sums as hwin, hand-interleaved (this order keeps the
-        // 10-row w = 5 kernel within 128 VGPRs without spills)
-        const float au = from_left(pu) + pu;
-        const float av = from_left(pv) + pv;
-        const float bu = from_left(uo) + pu;
-        const float bv = from_left(vo) + pv;
-        hue = launder_f(au + from_right(ue));
-        hve = launder_f(av + from_right(ve));
-        huo = launder_f(bu + from_right(pu));
-        hvo = launder_f(bv + from_right(pv));
-    } else if constexpr (W == 3) {
-        hue = launder_f(from_left(uo) + pu);
-        hve = launder_f(from_left(vo) + pv);
-        huo = launder_f(pu + from_right(ue));
-        hvo = launder_f(pv + from_right(ve));
-    } else {
-        hue = hwin<A, AR, 0>(ue, uo, pu);
-        hve = hwin<A, AR, 0>(ve, vo, pv);
-        huo = hwin<A, AR, 1>(ue, uo, pu);
-        hvo = hwin<A, AR, 1>(ve, vo, pv);
-    }
-}
 
 // workgroup-kernel geometry per window: slab rows per wave (deeper register
 // rings for wider windows) and double-buffered slab exchange while two
@@ -654,11 +524,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                 iyo, ito);
                 }
             }
-            const float se = __builtin_amdgcn_rsqf(p.alpha2 + ixe * ixe + iye * iye);
-            const float so = __builtin_amdgcn_rsqf(p.alpha2 + ixo * ixo + iyo * iyo);
-            X[r] = f2v{ixe * se, ixo * so};
-            Y[r] = f2v{iye * se, iyo * so};
-            T[r] = f2v{ite * se, ito * so};
+            op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);
         }
     }
 
@@ -758,10 +624,8 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                         sv = sv + hv[sh];
                     }
                 }
-                const f2v ub = su * invv, vb = sv * invv;
-                const f2v xv = X[y], yv = Y[y];
-                const f2v k = xv * ub + (yv * vb + T[y]);
-                f2v nu = ub - xv * k, nv = vb - yv * k;
+                f2v nu, nv;
+                op_update(su, sv, invv, X[y], Y[y], T[y], nu, nv);
                 if constexpr (EDGE) {
                     // outside the image u = v = 0 (BORDER_CONSTANT)
                     const bool rin = (rowmask >> y) & 1ull;
