@@ -41,6 +41,17 @@ namespace {
 
 thread_local std::string g_err;  // errors from calls without a context
 int g_kb_override = 0;
+// Jacobi pass kernel: 0 = automatic, 2 = K2 tiles, 3 = K3 streaming strips
+// (hsflow_set_jacobi_kernel; HSFLOW_JACOBI sets the process default)
+int g_kernel_override = -1;
+
+int jacobi_kernel_choice() {
+    if (g_kernel_override < 0) {
+        const char *e = getenv("HSFLOW_JACOBI");
+        g_kernel_override = e ? atoi(e) : 0;
+    }
+    return g_kernel_override;
+}
 
 int fail(hsflow_ctx *ctx, int code, const char *fmt, ...) {
     char buf[512];
@@ -278,7 +289,12 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         a.v_in = src_v;
         a.u_out = dst_is_user(pass) ? u : w.u2;
         a.v_out = dst_is_user(pass) ? v : w.v2;
-        hipError_t e = hsflow::launch_jacobi(a, window, kb, s);
+        // K3 and K2 give identical bits, so passes may mix (K3 runs full
+        // passes of even-width images only)
+        const int kc = jacobi_kernel_choice();
+        const bool k3 = kc == 3 && a.iters == kb && hsflow::k3_supported(window, kb, cols);
+        hipError_t e = k3 ? hsflow::launch_jacobi_stream(a, window, kb, s)
+                          : hsflow::launch_jacobi(a, window, kb, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "jacobi launch");
         src_u = a.u_out;
         src_v = a.v_out;
@@ -606,6 +622,12 @@ size_t hsflow_workspace_bytes(int rows, int cols, int batch) {
 int hsflow_set_iters_per_launch(int k) {
     if (k < 0) return HSFLOW_ERR_ARG;
     g_kb_override = k;
+    return HSFLOW_OK;
+}
+
+int hsflow_set_jacobi_kernel(int k) {
+    if (k != 0 && k != 2 && k != 3) return HSFLOW_ERR_ARG;
+    g_kernel_override = k;
     return HSFLOW_OK;
 }
 

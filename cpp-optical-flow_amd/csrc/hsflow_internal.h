@@ -20,12 +20,16 @@ struct JacobiArgs {
     int ablate;                // diagnostics only (HSFLOW_ABLATE): 1 = no
                                // iterations (memory only), 2 = no memory
                                // traffic (descriptors of size 0)
+    int seg_rows;              // K3: output rows per segment (launcher)
 };
 
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
                             int cols, int batch, uint32_t *gpack, float *gx, float *gy,
                             float *gt, uint32_t *flags, hipStream_t s);
 hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s);
+// K3 streaming pass (hsflow_stream.hip): exactly KB iterations, even widths
+hipError_t launch_jacobi_stream(JacobiArgs a, int W, int KB, hipStream_t s);
+bool k3_supported(int W, int KB, int cols);
 // config 5 pyramid (hsflow_pyramid.hip); dtype as HSFLOW_U8/F32/F16
 hipError_t launch_pyrdown(const void *src, int dtype, int rows, int cols, int batch,
                           float *dst, const uint32_t *flags, hipStream_t s);

@@ -356,7 +356,8 @@ __global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
 constexpr int wg_rows(int W) { return W <= 5 ? 10 : (W <= 7 ? 8 : 7); }
 constexpr bool wg_double_buffer(int W) { return W <= 5; }
 
-template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32>
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32,
+          bool ROWE = true>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[wg_double_buffer(W) ? 2 : 1][NW][W - 1][2][64],
                                         int tx, int ty, int wv, int lane, size_t pbase,
@@ -418,6 +419,10 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
         if (interior)
             wg_body<W, KB, RW, NW, SB, false, true, false>(p, xch, tx, ty, wv, lane, pbase,
                                                            plane_bytes);
+        else if (W <= 7 && ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows)
+            // left/right border tiles: every region row inside the image
+            wg_body<W, KB, RW, NW, SB, true, true, false, false>(p, xch, tx, ty, wv, lane,
+                                                                 pbase, plane_bytes);
         else
             wg_body<W, KB, RW, NW, SB, true, true, false>(p, xch, tx, ty, wv, lane, pbase,
                                                           plane_bytes);
@@ -427,7 +432,7 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     }
 }
 
-template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32>
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32, bool ROWE>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[wg_double_buffer(W) ? 2 : 1][NW][W - 1][2][64],
                                         int tx, int ty, int wv, int lane, size_t pbase,
@@ -443,6 +448,8 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
     const int r0 = ty * OY - HL + wv * RW;    // image row of slab row 0
     const bool ce = (unsigned)gce < (unsigned)cols;
     const bool co = (unsigned)(gce + 1) < (unsigned)cols;
+    // window-mean factor of this lane's columns: 1/w^2 inside the image, 0 outside
+    const f2v colm = {ce ? p.inv_w2 : 0.f, co ? p.inv_w2 : 0.f};
     const int ce_i = ce ? 1 : 0, co_i = co ? 1 : 0;
     uint64_t rowmask = 0;
 #pragma unroll
@@ -625,9 +632,10 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                     }
                 }
                 f2v nu, nv;
-                op_update(su, sv, invv, X[y], Y[y], T[y], nu, nv);
-                if constexpr (EDGE) {
-                    // outside the image u = v = 0 (BORDER_CONSTANT)
+                if constexpr (EDGE && W >= 8) {
+                    // outside the image u = v = 0 (BORDER_CONSTANT); per-lane
+                    // selects (the factor form below spills at W = 8, 9)
+                    op_update(su, sv, invv, X[y], Y[y], T[y], nu, nv);
                     const bool rin = (rowmask >> y) & 1ull;
                     const bool ie = rin & (launder(ce_i) != 0);
                     const bool io = rin & (launder(co_i) != 0);
@@ -635,6 +643,19 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                     nu.y = io ? nu.y : 0.f;
                     nv.x = ie ? nv.x : 0.f;
                     nv.y = io ? nv.y : 0.f;
+                } else if constexpr (EDGE) {
+                    // Outside the image u = v = 0 (BORDER_CONSTANT).  Columns:
+                    // the window mean is taken with factor 0 there and the
+                    // gradients read there are 0 (out-of-range loads), so the
+                    // update yields 0 (every value in the region is finite)
+                    // without per-lane masks.  Rows (wave-uniform): select.
+                    op_update(su, sv, launder_v2(colm), X[y], Y[y], T[y], nu, nv);
+                    if (ROWE && !((rowmask >> y) & 1ull)) {
+                        nu = f2v{0.f, 0.f};
+                        nv = f2v{0.f, 0.f};
+                    }
+                } else {
+                    op_update(su, sv, invv, X[y], Y[y], T[y], nu, nv);
                 }
                 U[y] = nu;
                 V[y] = nv;

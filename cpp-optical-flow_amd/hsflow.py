@@ -50,6 +50,7 @@ EXPORTS = (
     "hsflow_pyramid_level_size", "hsflow_pyramid_workspace_bytes",
     "hsflow_flow_pyramid_device", "hsflow_flow_pyramid", "hsflow_bgr_to_gray_device",
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
+    "hsflow_set_jacobi_kernel",
 )
 
 
@@ -106,6 +107,7 @@ def lib():
     L.hsflow_set_iters_per_launch.argtypes = [i]
     L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
     L.hsflow_set_max_streams.argtypes = [i]
+    L.hsflow_set_jacobi_kernel.argtypes = [i]
     L.hsflow_pyramid_level_size.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
     L.hsflow_pyramid_workspace_bytes.argtypes = [i, i, i, i]
     L.hsflow_pyramid_workspace_bytes.restype = _sz
@@ -467,6 +469,11 @@ def set_iters_per_launch(k: int):
 def set_max_streams(n: int):
     """Side streams a batch is split over (1 = off, 0 = default)."""
     _check(lib().hsflow_set_max_streams(int(n)))
+
+
+def set_jacobi_kernel(k: int):
+    """Jacobi pass kernel: 0 = automatic, 2 = K2 tiles, 3 = K3 streaming."""
+    _check(lib().hsflow_set_jacobi_kernel(int(k)))
 
 
 def iters_per_launch(rows, cols, batch, window) -> int:

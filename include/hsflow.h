@@ -119,6 +119,12 @@ int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
 int hsflow_set_iters_per_launch(int k);
 int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
 
+/* Kernel of the Jacobi passes: 0 = automatic (default, or HSFLOW_JACOBI),
+ * 2 = K2 register tiles, 3 = K3 streaming strips (full passes of even-width
+ * images; other passes fall back to K2).  Both give identical bits.
+ * Process-wide; not thread-safe against running solves. */
+int hsflow_set_jacobi_kernel(int k);
+
 /* Batches of >= 2 pairs are split over up to n side streams (forked from and
  * joined back to the caller's stream with events) so that concurrent Jacobi
  * launches overlap.  1 disables; 0 restores the default (2, or
