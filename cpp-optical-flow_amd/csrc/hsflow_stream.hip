@@ -44,6 +44,12 @@
 #ifndef K3_PF
 #define K3_PF 0
 #endif
+#ifndef K3_DECOUPLE  // 1: every stage boundary is a one-step hand-off
+#define K3_DECOUPLE 0
+#endif
+#ifndef K3_LATE_OPS  // 1: read each stage's operator row just before it
+#define K3_LATE_OPS 1
+#endif
 #ifndef K3_STEP_FENCE
 #define K3_STEP_FENCE 1
 #endif
@@ -61,7 +67,9 @@ struct K3Geo {
     // step s-1 (stage 1: the row loaded at step s), so within a step every
     // stage is an independent dependency chain.  Input row lag D(k) and
     // output row lag LAG(k) behind the newest loaded row:
-    static constexpr int D(int k) { return (AR + 1) * (k - 1); }
+    static constexpr int D(int k) {
+        return K3_DECOUPLE ? (AR + 1) * (k - 1) : AR * (k - 1) + (k - 1) / KPW;
+    }
     static constexpr int LAG(int k) { return D(k) + AR; }
     // Operator ring rows: every stage reads its output row's (X, Y, T) from
     // the ring, except the very last one, which reuses the row stage KB-1
@@ -69,6 +77,8 @@ struct K3Geo {
     // only up to LAG(KB-1).
     static constexpr int LMAX = KB >= 2 ? LAG(KB - 1) : LAG(KB);
     static constexpr int R = LMAX + 1;
+    // steps between stage KB-1's read of a row and stage KB's use of it
+    static constexpr int GAP = KB >= 2 ? LAG(KB) - LAG(KB - 1) : 1;
     static constexpr int P = (W % 2 == 0) ? W : 2 * W;  // unroll period
     // load distance in rows (5 rows measured no faster than 2 and costs 18
     // VGPRs; K3_PF overrides for experiments)
@@ -122,9 +132,10 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
         for (int w = 0; w < W; ++w) hu[i][w] = hv[i][w] = qu[i][w] = qv[i][w] = f2v{0.f, 0.f};
     }
     // last stage's operator rows: AR+1 deep shift register
-    f2v DX[kDelay ? AR + 1 : 1], DY[kDelay ? AR + 1 : 1], DT[kDelay ? AR + 1 : 1];
+    constexpr int GAP = G::GAP;
+    f2v DX[GAP], DY[GAP], DT[GAP];
 #pragma unroll
-    for (int d = 0; d < (kDelay ? AR + 1 : 1); ++d) DX[d] = DY[d] = DT[d] = f2v{0.f, 0.f};
+    for (int d = 0; d < GAP; ++d) DX[d] = DY[d] = DT[d] = f2v{0.f, 0.f};
 
     // wave 0: load queue of PF rows
     u2v qU[PF], qV[PF], qG[PF], qX[G32 ? PF : 1], qY[G32 ? PF : 1], qT[G32 ? PF : 1];
@@ -198,11 +209,13 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
             const int s = sb + ph;
             if (s >= nsteps) break;
             const int rbase = s % R;  // ring slot of relative row s
+#if !K3_LATE_OPS
             fetch_ops(s);
+#endif
             if constexpr (kDelay) {
-                Xk[KPW - 1] = DX[AR];
-                Yk[KPW - 1] = DY[AR];
-                Tk[KPW - 1] = DT[AR];
+                Xk[KPW - 1] = DX[GAP - 1];
+                Yk[KPW - 1] = DY[GAP - 1];
+                Tk[KPW - 1] = DT[GAP - 1];
             }
             // first stage's input row
             f2v in_u, in_v;
@@ -243,8 +256,8 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
 #pragma unroll
             for (int i = 0; i < KPW; ++i) {
                 const int k = J * KPW + i + 1;  // global stage index
-                const f2v xu = i == 0 ? in_u : ou[i - 1];
-                const f2v xv = i == 0 ? in_v : ov[i - 1];
+                const f2v xu = i == 0 ? in_u : (K3_DECOUPLE ? ou[i - 1] : nu[i - 1]);
+                const f2v xv = i == 0 ? in_v : (K3_DECOUPLE ? ov[i - 1] : nv[i - 1]);
                 // relative input row t = s - D(k); ring slots by t mod W
                 const int sl = k3_mod(ph - G::D(k), W);
                 const int sp = k3_mod(ph - G::D(k) - 1, W);
@@ -279,6 +292,18 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
                         sv = sv + hv[i][sh];
                     }
                 }
+#if K3_LATE_OPS
+                if (!(kDelay && k == KB)) {
+                    int ys = rbase - G::LAG(k);
+                    ys += ys < 0 ? R : 0;
+                    const float2 x2 = L.xyt[ys][0][lane];
+                    const float2 y2 = L.xyt[ys][1][lane];
+                    const float2 t2 = L.xyt[ys][2][lane];
+                    Xk[i] = f2v{x2.x, x2.y};
+                    Yk[i] = f2v{y2.x, y2.y};
+                    Tk[i] = f2v{t2.x, t2.y};
+                }
+#endif
                 f2v m = colm;
                 if constexpr (RE) {
                     const int yabs = r0 + s - G::LAG(k);
@@ -294,7 +319,7 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
             if constexpr (kDelay) {
                 // stage KB-1's row this step is stage KB's row AR+1 steps on
 #pragma unroll
-                for (int d = AR; d > 0; --d) {
+                for (int d = GAP - 1; d > 0; --d) {
                     DX[d] = DX[d - 1];
                     DY[d] = DY[d - 1];
                     DT[d] = DT[d - 1];
@@ -354,7 +379,7 @@ __device__ __forceinline__ void k3_dispatch(const JacobiArgs &p, K3Lds<W, KB, S>
 }
 
 template <int W, int KB, int S>
-__global__ __launch_bounds__(S * 64) void hs_jacobi_stream_kernel(const JacobiArgs p) {
+__global__ __launch_bounds__(S * 64, 4) void hs_jacobi_stream_kernel(const JacobiArgs p) {
     using G = K3Geo<W, KB, S>;
     __shared__ K3Lds<W, KB, S> L;
     // XCD-aware workgroup order (see hs_jacobi_kernel): each XCD walks a
@@ -388,7 +413,7 @@ template <int W, int KB, int S>
 static hipError_t launch_k3(JacobiArgs a, hipStream_t s) {
     using G = K3Geo<W, KB, S>;
     a.tiles_x = (a.cols + G::OX - 1) / G::OX;  // strips
-    // Segment height: one round of resident workgroups (6 per CU) when the
+    // Segment height: one round of resident workgroups when the
     // batch is small, else whole-strip segments.  HSFLOW_SEG overrides.
     static const int seg_env = [] {
         const char *e = getenv("HSFLOW_SEG");
@@ -399,7 +424,16 @@ static hipError_t launch_k3(JacobiArgs a, hipStream_t s) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess)
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const long slots = 6L * cus;
+        // resident workgroups per CU (LDS and VGPR limited)
+        static const int per_cu = [] {
+            int n = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &n, reinterpret_cast<const void *>(&hs_jacobi_stream_kernel<W, KB, S>),
+                    S * 64, 0) != hipSuccess || n <= 0)
+                n = 4;
+            return n;
+        }();
+        const long slots = (long)per_cu * cus;
         const long strips = (long)a.tiles_x * a.batch;
         long nseg = strips >= slots ? 1 : slots / strips;
         if (nseg < 1) nseg = 1;
