@@ -52,6 +52,15 @@ def test_iters_per_launch_policy():
     hsflow.set_iters_per_launch(0)
 
 
+def test_jacobi_kernel_selector():
+    """0 = automatic, 2 = K2 tiles, 3 = K3 streaming strips; others rejected."""
+    for bad in (-1, 1, 4, 99):
+        with pytest.raises(hsflow.HsflowError):
+            hsflow.set_jacobi_kernel(bad)
+    for k in (2, 3, 0):
+        hsflow.set_jacobi_kernel(k)
+
+
 def test_device_entry_points_validate_before_touching_the_gpu():
     L = hsflow.lib()
     # bad sizes / null pointers are rejected without any HIP call
