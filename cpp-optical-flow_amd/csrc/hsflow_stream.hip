@@ -41,7 +41,8 @@
 #include "hsflow_device.h"
 #include "hsflow_internal.h"
 
-#ifndef K3_PF
+// Build-time experiment switches (measured alternatives):
+#ifndef K3_PF  // load distance in rows (0: default 2)
 #define K3_PF 0
 #endif
 #ifndef K3_DECOUPLE  // 1: every stage boundary is a one-step hand-off
@@ -49,9 +50,6 @@
 #endif
 #ifndef K3_LATE_OPS  // 1: read each stage's operator row just before it
 #define K3_LATE_OPS 1
-#endif
-#ifndef K3_STEP_FENCE
-#define K3_STEP_FENCE 1
 #endif
 
 namespace hsflow {
@@ -359,7 +357,7 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
             // wave 0's loads in flight)
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
             if (p.ablate != 4) __builtin_amdgcn_s_barrier();
-            if (K3_STEP_FENCE) __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -368,9 +366,6 @@ template <int W, int KB, int S, bool G32, bool RE, int J = 0>
 __device__ __forceinline__ void k3_dispatch(const JacobiArgs &p, K3Lds<W, KB, S> &L, int wv,
                                             int lane, int pair, int strip, int seg) {
     if constexpr (J < S) {
-#ifdef K3_ONLY_ROLE
-        if (J != K3_ONLY_ROLE) { k3_dispatch<W, KB, S, G32, RE, J + 1>(p, L, wv, lane, pair, strip, seg); return; }
-#endif
         if (wv == J)
             k3_role<W, KB, S, G32, RE, J>(p, L, lane, pair, strip, seg);
         else
