@@ -91,3 +91,62 @@ def test_single_rank_path():
     out = fp.run_stream(stream, N_PAIRS, (ROWS, COLS), torch.float32, _solve,
                         torch.device("cpu"), 0, 1)
     assert len(out) == N_PAIRS
+
+
+# ---- the same protocol with the real HIP solver (2 processes, one GPU) ----
+
+def _gpu_solve(I0, I1):
+    import hsflow
+    u, v = hsflow.flow_device(I0.cuda(), I1.cuda(), 5, 30, 1.0)
+    torch.cuda.synchronize()
+    return u.cpu(), v.cpu()
+
+
+G_ROWS, G_COLS, G_PAIRS = 96, 258, 5
+
+
+def _gpu_stream():
+    return [tuple(torch.from_numpy(a) for a in synth_pair(2000 + j, G_ROWS, G_COLS))
+            for j in range(G_PAIRS)]
+
+
+def _gpu_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [here, os.path.join(root, "oracle"), os.path.join(root, "cpp-optical-flow_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # transport over gloo with host tensors (both ranks share the box's one
+    # GPU); each rank solves its pairs with libhsflow on cuda:0
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        stream = _gpu_stream() if rank == 0 else None
+        out = fp.run_stream(stream, G_PAIRS, (G_ROWS, G_COLS), torch.float32, _gpu_solve,
+                            torch.device("cpu"), rank, world)
+        q.put(("ok", [(u.numpy(), v.numpy()) for (u, v) in out]) if rank == 0
+              else ("peer", None))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_frame_parallel_gpu_solver_world2_bit_identical():
+    """pairs solved on two ranks (each through the C ABI on
+    the GPU) and gathered to rank 0 equal a single-rank solve bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=110) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    assert all(r[0] != "err" for r in res), res
+    flows = [r for r in res if r[0] == "ok"][0][1]
+    assert len(flows) == G_PAIRS
+    for j, (I0, I1) in enumerate(_gpu_stream()):
+        u, v = _gpu_solve(I0, I1)
+        assert np.array_equal(flows[j][0], u.numpy()) and np.array_equal(flows[j][1], v.numpy())
