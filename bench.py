@@ -236,7 +236,11 @@ def main():
                          "algorithmic_B_per_px_iter": 28,
                          "compulsory_bytes_per_launch": int(compulsory),
                          "compulsory_GBps": round(compulsory_gbps, 1),
-                         "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4)},
+                         "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4),
+                         # measured (DESIGN.md §4 Roofline): the pass is bound
+                         # by VALU issue, its compute phase at ~95 % of the
+                         # wave64 VALU rate; HBM is the nominal SURVEY class
+                         "limiter": "valu"},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "sane": ok,
