@@ -383,12 +383,22 @@ def test_cpp_main_driver_reproduces_reference_plot(tmp_path, tag):
     assert norm_rel_err(u, uo) <= TOL
 
 
+@pytest.mark.parametrize("kernel", [0, 3])  # automatic (K2), K3 streaming strips
 @pytest.mark.parametrize("batch", [1, 3])
-def test_device_solve_captures_into_a_hip_graph(hs, batch):
+def test_device_solve_captures_into_a_hip_graph(hs, batch, kernel):
     """include/hsflow.h: the *_device calls are stream-ordered and never
     allocate or synchronise, so a whole solve (K1, the K2 passes, the batch
     split over side streams with event fork/join) can be captured into a
     hipGraph and replayed; the replay gives the eager result bit for bit."""
+    import torch
+    hs.set_jacobi_kernel(kernel)
+    try:
+        _capture_and_replay(hs, batch)
+    finally:
+        hs.set_jacobi_kernel(0)
+
+
+def _capture_and_replay(hs, batch):
     import torch
     pairs = [hs.synth_pair(1500 + k, 120, 210) for k in range(batch)]
     t0 = torch.stack([torch.from_numpy(p[0]) for p in pairs]).cuda()
