@@ -355,11 +355,18 @@ __global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
 // workgroups' W-1 boundary rows fit in LDS
 constexpr int wg_rows(int W) { return W <= 5 ? 10 : (W <= 7 ? 8 : 7); }
 constexpr bool wg_double_buffer(int W) { return W <= 5; }
+// T plane in LDS (w = 5, 12-row slabs): frees 2 VGPRs per row for taller
+// slabs; the exchange is single-buffered so two workgroups still fit a CU
+// (32 KB exchange + 48 KB T plane each)
+constexpr bool wg_tlds(int W, int RW) { return W == 5 && RW > 10; }
+constexpr int wg_nbuf(int W, int RW) {
+    return (wg_double_buffer(W) && !wg_tlds(W, RW)) ? 2 : 1;
+}
 
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32,
           bool ROWE = true>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
-                                        float2 (&xch)[wg_double_buffer(W) ? 2 : 1][NW][W - 1][2][64],
+                                        float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64], float2 *tpl,
                                         int tx, int ty, int wv, int lane, size_t pbase,
                                         int plane_bytes);
 
@@ -377,7 +384,8 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     static_assert(OX > 0 && OY > 0 && (OX % 2) == 0, "geometry");
     static_assert(RW <= 64, "row mask is 64 bits");
     // [parity][wave][boundary row][field u/v][lane] of (even, odd) columns
-    __shared__ float2 xch[wg_double_buffer(W) ? 2 : 1][NW][NB][2][64];
+    __shared__ float2 xch[wg_nbuf(W, RW)][NW][NB][2][64];
+    __shared__ float2 tpl[wg_tlds(W, RW) ? NW * RW * 64 : 1];
 
     // XCD-aware workgroup order (see hs_jacobi_kernel)
     const int nblk = gridDim.x * gridDim.y;
@@ -408,33 +416,33 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
     if (g32) {
         if ((cols & 1) == 0)
-            wg_body<W, KB, RW, NW, SB, true, true, true>(p, xch, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, true, true, true>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                          plane_bytes);
         else
-            wg_body<W, KB, RW, NW, SB, true, false, true>(p, xch, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, true, false, true>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                           plane_bytes);
         return;
     }
     if ((cols & 1) == 0) {
         if (interior)
-            wg_body<W, KB, RW, NW, SB, false, true, false>(p, xch, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, false, true, false>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                            plane_bytes);
         else if (W <= 7 && ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows)
             // left/right border tiles: every region row inside the image
-            wg_body<W, KB, RW, NW, SB, true, true, false, false>(p, xch, tx, ty, wv, lane,
-                                                                 pbase, plane_bytes);
+            wg_body<W, KB, RW, NW, SB, true, true, false, false>(p, xch, tpl, tx, ty, wv,
+                                                                 lane, pbase, plane_bytes);
         else
-            wg_body<W, KB, RW, NW, SB, true, true, false>(p, xch, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, true, true, false>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                           plane_bytes);
     } else {
-        wg_body<W, KB, RW, NW, SB, true, false, false>(p, xch, tx, ty, wv, lane, pbase,
+        wg_body<W, KB, RW, NW, SB, true, false, false>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                        plane_bytes);
     }
 }
 
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32, bool ROWE>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
-                                        float2 (&xch)[wg_double_buffer(W) ? 2 : 1][NW][W - 1][2][64],
+                                        float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64], float2 *tpl,
                                         int tx, int ty, int wv, int lane, size_t pbase,
                                         int plane_bytes) {
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
@@ -484,7 +492,9 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
     //   u' = ubar - X (X ubar + Y vbar + T),  v' = vbar - Y (...)
     // which is hornSchunck.cpp:63-73 rearranged (c = (Ix ubar + Iy vbar +
     // It)/D): 6 packed ops per column pair and no unpack / rcp per iteration.
-    f2v U[RW], V[RW], X[RW], Y[RW], T[RW];
+    constexpr bool TL = wg_tlds(W, RW);
+    f2v U[RW], V[RW], X[RW], Y[RW], T[TL ? 1 : RW];
+    float2 *tw = tpl + (TL ? wv * RW * 64 + lane : 0);  // this lane's T rows
     {
         const int off0 = (r0 * cols + gce) * 4;
 #pragma unroll
@@ -531,12 +541,26 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                 iyo, ito);
                 }
             }
-            op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);
+            if constexpr (TL) {
+                f2v Tr;
+                op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], Tr);
+                tw[r * 64] = make_float2(Tr.x, Tr.y);
+            } else {
+                op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);
+            }
         }
     }
 
     const float inv = p.inv_w2;
     const f2v invv = {inv, inv};
+    auto t_row = [&](int y) -> f2v {
+        if constexpr (TL) {
+            const float2 t = tw[y * 64];
+            return f2v{t.x, t.y};
+        } else {
+            return T[y];
+        }
+    };
     // horizontal sums of slab row t (own data)
     auto hrow = [&](int t, f2v &hu, f2v &hv) {
         float a, b, c, d;
@@ -547,7 +571,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
 
     const int n_it = p.ablate == 1 ? 0 : p.iters;
     for (int it = 0; it < n_it; ++it) {
-        const int par = wg_double_buffer(W) ? (it & 1) : 0;
+        const int par = wg_nbuf(W, RW) == 2 ? (it & 1) : 0;
         // 1. horizontal sums of the boundary rows first, published for the
         //    neighbouring slabs: rows 0..AR-1 feed the wave above, rows
         //    RW-A..RW-1 the wave below.  Exchanging sums (not raw rows)
@@ -635,7 +659,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                 if constexpr (EDGE && W >= 8) {
                     // outside the image u = v = 0 (BORDER_CONSTANT); per-lane
                     // selects (the factor form below spills at W = 8, 9)
-                    op_update(su, sv, invv, X[y], Y[y], T[y], nu, nv);
+                    op_update(su, sv, invv, X[y], Y[y], t_row(y), nu, nv);
                     const bool rin = (rowmask >> y) & 1ull;
                     const bool ie = rin & (launder(ce_i) != 0);
                     const bool io = rin & (launder(co_i) != 0);
@@ -649,13 +673,13 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                     // gradients read there are 0 (out-of-range loads), so the
                     // update yields 0 (every value in the region is finite)
                     // without per-lane masks.  Rows (wave-uniform): select.
-                    op_update(su, sv, launder_v2(colm), X[y], Y[y], T[y], nu, nv);
+                    op_update(su, sv, launder_v2(colm), X[y], Y[y], t_row(y), nu, nv);
                     if (ROWE && !((rowmask >> y) & 1ull)) {
                         nu = f2v{0.f, 0.f};
                         nv = f2v{0.f, 0.f};
                     }
                 } else {
-                    op_update(su, sv, invv, X[y], Y[y], T[y], nu, nv);
+                    op_update(su, sv, invv, X[y], Y[y], t_row(y), nu, nv);
                 }
                 U[y] = nu;
                 V[y] = nv;
@@ -664,7 +688,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
         }
         // single-buffered exchange: the neighbours' reads of this iteration
         // must finish before the next iteration's publish overwrites them
-        if constexpr (!wg_double_buffer(W)) __syncthreads();
+        if constexpr (wg_nbuf(W, RW) == 1) __syncthreads();
     }
 
     // interior tile: workgroup rows [HL, HL + OY), lanes [HLc/2, (HLc + OX)/2)
@@ -853,6 +877,16 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     // per CU).  SB = 16 > rows swept: no scheduling barriers inside the
     // sweep, so the scheduler interleaves rows and fills the DPP
     // read-after-write wait states.
+    // w = 5, KB <= 6: 11-row slabs (88 x 128 region) with the T plane in
+    // LDS and a single-buffered exchange: same box, 1080p x 8 / 4K x 2,
+    // 1.011 M / 1.072 M -> 1.032 M / 1.089 M Mpix*iter/s (12 rows spill).
+    // HSFLOW_K2_ROWS=10 keeps the all-register 10-row slabs.
+    static const int rows_env = [] {
+        const char *e = getenv("HSFLOW_K2_ROWS");
+        return e ? atoi(e) : 0;
+    }();
+    if constexpr (W == 5 && KB * (W - 1) <= 24)
+        if (rows_env != 10) return launch_jacobi_wg<W, KB, 11, 8, 16>(a, s);
     return launch_jacobi_wg<W, KB, wg_rows(W), 8, 16>(a, s);
     }
 }
