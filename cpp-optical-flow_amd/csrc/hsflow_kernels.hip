@@ -358,9 +358,10 @@ constexpr bool wg_double_buffer(int W) { return W <= 5; }
 // T plane in LDS (w = 5, 12-row slabs): frees 2 VGPRs per row for taller
 // slabs; the exchange is single-buffered so two workgroups still fit a CU
 // (32 KB exchange + 48 KB T plane each)
-constexpr bool wg_tlds(int W, int RW) { return W == 5 && RW > 10; }
+// (w = 3 keeps the double-buffered exchange: 2 boundary rows, 32 KB + 44 KB)
+constexpr bool wg_tlds(int W, int RW) { return (W == 3 || W == 5) && RW > 10; }
 constexpr int wg_nbuf(int W, int RW) {
-    return (wg_double_buffer(W) && !wg_tlds(W, RW)) ? 2 : 1;
+    return (wg_double_buffer(W) && !(W == 5 && wg_tlds(W, RW))) ? 2 : 1;
 }
 
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32,
@@ -885,8 +886,9 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
         const char *e = getenv("HSFLOW_K2_ROWS");
         return e ? atoi(e) : 0;
     }();
-    if constexpr (W == 5 && KB * (W - 1) <= 24)
-        if (rows_env != 10) return launch_jacobi_wg<W, KB, 11, 8, 16>(a, s);
+    if constexpr ((W == 5 || W == 3) && KB * (W - 1) <= 24)
+        if (rows_env != 10 && (W == 5 || rows_env == 11))
+            return launch_jacobi_wg<W, KB, 11, 8, 16>(a, s);
     return launch_jacobi_wg<W, KB, wg_rows(W), 8, 16>(a, s);
     }
 }
