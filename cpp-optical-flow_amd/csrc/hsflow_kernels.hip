@@ -358,10 +358,16 @@ constexpr bool wg_double_buffer(int W) { return W <= 5; }
 // T plane in LDS (w = 5, 12-row slabs): frees 2 VGPRs per row for taller
 // slabs; the exchange is single-buffered so two workgroups still fit a CU
 // (32 KB exchange + 48 KB T plane each)
-// (w = 3 keeps the double-buffered exchange: 2 boundary rows, 32 KB + 44 KB)
-constexpr bool wg_tlds(int W, int RW) { return (W == 3 || W == 5) && RW > 10; }
+// Any slab taller than the all-register height wg_rows(W) keeps T in LDS.
+// (w = 3 keeps the double-buffered exchange: 2 boundary rows, 32 KB + 44 KB.)
+constexpr bool wg_tlds(int W, int RW) { return RW > wg_rows(W); }
 constexpr int wg_nbuf(int W, int RW) {
-    return (wg_double_buffer(W) && !(W == 5 && wg_tlds(W, RW))) ? 2 : 1;
+    return (wg_double_buffer(W) && !(W >= 4 && wg_tlds(W, RW))) ? 2 : 1;
+}
+// slab height of the T-in-LDS variant (two workgroups per CU must fit the
+// 160 KB LDS: exchange + 8 RW rows x 512 B of T); 0 = none
+constexpr int wg_rows_tl(int W) {
+    return (W == 3 || W == 4 || W == 5) ? 11 : (W == 6 ? 10 : 0);
 }
 
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32,
@@ -878,17 +884,22 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     // per CU).  SB = 16 > rows swept: no scheduling barriers inside the
     // sweep, so the scheduler interleaves rows and fills the DPP
     // read-after-write wait states.
-    // w = 5, KB <= 6: 11-row slabs (88 x 128 region) with the T plane in
-    // LDS and a single-buffered exchange: same box, 1080p x 8 / 4K x 2,
-    // 1.011 M / 1.072 M -> 1.032 M / 1.089 M Mpix*iter/s (12 rows spill).
-    // HSFLOW_K2_ROWS=10 keeps the all-register 10-row slabs.
-    static const int rows_env = [] {
-        const char *e = getenv("HSFLOW_K2_ROWS");
-        return e ? atoi(e) : 0;
+    // Taller slabs with the T plane in LDS (wg_rows_tl): w = 5, 11 rows
+    // (88 x 128 region), single-buffered exchange: same box, 1080p x 8 /
+    // 4K x 2, 1.011 M / 1.072 M -> 1.032 M / 1.089 M Mpix*iter/s (12 rows
+    // spill).  HSFLOW_K2_TL=0 keeps the all-register slabs everywhere,
+    // =1 uses the taller ones for every window that has them; default w = 5
+    // and w = 6 (8 -> 10 rows: 1080p 782 k -> 859 k, 4K 793 k -> 891 k);
+    // at w = 3 and w = 4 they measure equal to the all-register slabs.
+    static const int tl_env = [] {
+        const char *e = getenv("HSFLOW_K2_TL");
+        return e ? atoi(e) : -1;
     }();
-    if constexpr ((W == 5 || W == 3) && KB * (W - 1) <= 24)
-        if (rows_env != 10 && (W == 5 || rows_env == 11))
-            return launch_jacobi_wg<W, KB, 11, 8, 16>(a, s);
+    constexpr int RT = wg_rows_tl(W);
+    if constexpr (RT > 0 && KB * (W - 1) < 8 * RT / 2) {
+        const bool on = tl_env < 0 ? (W == 5 || W == 6) : tl_env != 0;
+        if (on) return launch_jacobi_wg<W, KB, RT, 8, 16>(a, s);
+    }
     return launch_jacobi_wg<W, KB, wg_rows(W), 8, 16>(a, s);
     }
 }
