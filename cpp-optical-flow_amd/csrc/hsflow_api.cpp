@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hsflow.h"
@@ -35,6 +36,8 @@ struct hsflow_ctx {
     // pinned host staging for the f32 results
     float *h_stage = nullptr;
     size_t h_stage_bytes = 0;
+    // one event per staged plane of a download (created on first use)
+    hipEvent_t dl_ev[3] = {nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -421,24 +424,60 @@ int upload(hsflow_ctx *ctx, const void *src, int dtype, int rows, int cols, size
     return HSFLOW_OK;
 }
 
-// dense device f32 plane -> host rows of dtype_out with step `step`
-int download(hsflow_ctx *ctx, const float *src, int rows, int cols, void *dst,
-             int dtype_out, size_t step) {
+// f32 stage rows -> f64 host rows (the caller's CV_64FC1 buffer), split
+// over a few host threads: the writes first-touch the caller's freshly
+// allocated pages, which dominates a single-threaded conversion
+void widen_rows(const float *stage, int rows, int cols, void *dst, size_t step) {
+    auto run = [&](int r0, int r1) {
+        for (int r = r0; r < r1; ++r) {
+            double *d = (double *)((char *)dst + (size_t)r * step);
+            const float *s = stage + (size_t)r * cols;
+            for (int c = 0; c < cols; ++c) d[c] = (double)s[c];
+        }
+    };
+    const size_t px = (size_t)rows * cols;
+    unsigned hw = std::thread::hardware_concurrency();
+    int nt = (int)std::min<unsigned>(8u, hw ? hw : 1u);
+    if (px < (1u << 18) || nt <= 1 || rows < 2 * nt) {
+        run(0, rows);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const int per = (rows + nt - 1) / nt;
+    for (int t = 1; t < nt; ++t) {
+        const int r0 = t * per, r1 = std::min(rows, r0 + per);
+        if (r0 < r1) pool.emplace_back(run, r0, r1);
+    }
+    run(0, std::min(rows, per));
+    for (auto &th : pool) th.join();
+}
+
+// n dense device f32 planes -> host rows of dtype_out with step `step`.
+// f64: every plane's copy is queued into its own stage slot at once, and
+// plane k is widened while planes k+1.. are still in flight.
+int download_planes(hsflow_ctx *ctx, const float *const *src, void *const *dst, int n,
+                    int rows, int cols, int dtype_out, size_t step) {
     if (dtype_out == HSFLOW_F32) {
-        HIP_TRY(ctx, hipMemcpy2DAsync(dst, step, src, (size_t)cols * 4, (size_t)cols * 4,
-                                      rows, hipMemcpyDeviceToHost, ctx->stream));
+        for (int k = 0; k < n; ++k)
+            HIP_TRY(ctx, hipMemcpy2DAsync(dst[k], step, src[k], (size_t)cols * 4,
+                                          (size_t)cols * 4, rows, hipMemcpyDeviceToHost,
+                                          ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         return HSFLOW_OK;
     }
-    int rc = grow_host(ctx, (size_t)rows * cols * 4);
+    const size_t plane = (size_t)rows * cols;
+    int rc = grow_host(ctx, plane * 4 * n);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_stage, src, (size_t)rows * cols * 4,
-                                hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (int r = 0; r < rows; ++r) {
-        double *d = (double *)((char *)dst + (size_t)r * step);
-        const float *s = ctx->h_stage + (size_t)r * cols;
-        for (int c = 0; c < cols; ++c) d[c] = (double)s[c];
+    for (int k = 0; k < n; ++k) {
+        if (!ctx->dl_ev[k])
+            HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->dl_ev[k], hipEventDisableTiming));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_stage + k * plane, src[k], plane * 4,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(ctx->dl_ev[k], ctx->stream));
+    }
+    for (int k = 0; k < n; ++k) {
+        HIP_TRY(ctx, hipEventSynchronize(ctx->dl_ev[k]));
+        widen_rows(ctx->h_stage + k * plane, rows, cols, dst[k], step);
     }
     return HSFLOW_OK;
 }
@@ -604,6 +643,8 @@ void hsflow_destroy(hsflow_ctx *ctx) {
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    for (hipEvent_t e : ctx->dl_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -703,8 +744,12 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     rc = jacobi_impl(ctx, rows, cols, 1, window, iters, (float)alpha, false,
                      dt0 != HSFLOW_U8, du, dv, ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
-    if ((rc = download(ctx, du, rows, cols, u, dtype_out, out_step))) return rc;
-    if ((rc = download(ctx, dv, rows, cols, v, dtype_out, out_step))) return rc;
+    {
+        const float *srcs[2] = {du, dv};
+        void *dsts[2] = {u, v};
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
+            return rc;
+    }
     return HSFLOW_OK;
 }
 
@@ -804,8 +849,12 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
     rc = pyramid_impl(ctx, in0, in1, dt0, rows, cols, 1, levels, window, iters,
                       (float)alpha, du, dv, ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
-    if ((rc = download(ctx, du, rows, cols, u, dtype_out, out_step))) return rc;
-    if ((rc = download(ctx, dv, rows, cols, v, dtype_out, out_step))) return rc;
+    {
+        const float *srcs[2] = {du, dv};
+        void *dsts[2] = {u, v};
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
+            return rc;
+    }
     return HSFLOW_OK;
 }
 
@@ -858,8 +907,12 @@ int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, i
     rc = jacobi_impl(ctx, rows, cols, 1, window, iters, (float)alpha, false, false, du, dv,
                      ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
-    if ((rc = download(ctx, du, rows, cols, u, dtype_out, out_step))) return rc;
-    if ((rc = download(ctx, dv, rows, cols, v, dtype_out, out_step))) return rc;
+    {
+        const float *srcs[2] = {du, dv};
+        void *dsts[2] = {u, v};
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
+            return rc;
+    }
     return HSFLOW_OK;
 }
 
@@ -887,9 +940,12 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
     rc = gradients_impl(ctx, in0, in1, dt0, rows, cols, 1, dx, dy, dt, ctx->d_ws,
                         ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
-    if ((rc = download(ctx, dx, rows, cols, gx, dtype_out, out_step))) return rc;
-    if ((rc = download(ctx, dy, rows, cols, gy, dtype_out, out_step))) return rc;
-    if ((rc = download(ctx, dt, rows, cols, gt, dtype_out, out_step))) return rc;
+    {
+        const float *srcs[3] = {dx, dy, dt};
+        void *dsts[3] = {gx, gy, gt};
+        if ((rc = download_planes(ctx, srcs, dsts, 3, rows, cols, dtype_out, out_step)))
+            return rc;
+    }
     return HSFLOW_OK;
 }
 
