@@ -848,6 +848,29 @@ bool kb_supported(int W, int KB, bool need_f32) {
     return need_f32 ? kb_ok_f32(W, KB) : kb_ok_packed(W, KB);
 }
 
+// compute units of the current device (cached per device id)
+static int device_cus() {
+    static int per_dev[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (per_dev[dev] == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                hipSuccess || cus <= 0)
+            cus = 256;
+        per_dev[dev] = cus;
+    }
+    return per_dev[dev];
+}
+
+// workgroups of a workgroup-kernel launch with RW-row slabs (8 waves)
+static long wg_tiles(const JacobiArgs &a, int W, int KB, int RW) {
+    const int HL = KB * (W - W / 2 - 1), HR = KB * (W / 2);
+    const int ox = 128 - (HL + (HL & 1)) - (HR + (HR & 1));
+    const int oy = 8 * RW - KB * (W - 1);
+    return (long)((a.cols + ox - 1) / ox) * ((a.rows + oy - 1) / oy) * a.batch;
+}
+
 template <int W, int KB, int RW, int NW, int SB>
 static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     constexpr int HL = KB * (W - W / 2 - 1), HR = KB * (W / 2);
@@ -897,7 +920,16 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     }();
     constexpr int RT = wg_rows_tl(W);
     if constexpr (RT > 0 && KB * (W - 1) < 8 * RT / 2) {
-        const bool on = tl_env < 0 ? (W == 5 || W == 6) : tl_env != 0;
+        bool on = tl_env < 0 ? (W == 5 || W == 6) : tl_env != 0;
+        if (on && tl_env < 0) {
+            // Taller slabs mean fewer workgroups: keep them only while the
+            // launch still fills one round of 2 workgroups per CU (single
+            // 1080p pair at w = 5: 323 vs 380 workgroups for 512 slots,
+            // 515 k vs 569 k Mpix*iter/s with the all-register slabs).
+            const long slots = 2L * device_cus();
+            const long t_tall = wg_tiles(a, W, KB, RT), t_reg = wg_tiles(a, W, KB, wg_rows(W));
+            if (t_tall < slots && t_reg > t_tall) on = false;
+        }
         if (on) return launch_jacobi_wg<W, KB, RT, 8, 16>(a, s);
     }
     return launch_jacobi_wg<W, KB, wg_rows(W), 8, 16>(a, s);
