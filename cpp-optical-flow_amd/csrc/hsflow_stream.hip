@@ -61,17 +61,17 @@ struct K3Geo {
     static constexpr int HL = KB * A, HR = KB * AR;
     static constexpr int HLc = HL + (HL & 1), HRc = HR + (HR & 1);
     static constexpr int OX = 128 - HLc - HRc;  // output columns per strip
-    // Stage k (1..KB) consumes at step s the row its predecessor emitted at
-    // step s-1 (stage 1: the row loaded at step s), so within a step every
-    // stage is an independent dependency chain.  Input row lag D(k) and
-    // output row lag LAG(k) behind the newest loaded row:
+    // Stage k (1..KB) consumes the row its predecessor emitted in the same
+    // step when both are in one wave, and the row emitted one step earlier
+    // across a wave boundary (K3_DECOUPLE: at every boundary).  Input row
+    // lag D(k) and output row lag LAG(k) behind the newest loaded row:
     static constexpr int D(int k) {
         return K3_DECOUPLE ? (AR + 1) * (k - 1) : AR * (k - 1) + (k - 1) / KPW;
     }
     static constexpr int LAG(int k) { return D(k) + AR; }
     // Operator ring rows: every stage reads its output row's (X, Y, T) from
     // the ring, except the very last one, which reuses the row stage KB-1
-    // read AR+1 steps earlier (register delay line) -- the ring then spans
+    // read GAP steps earlier (register delay line) -- the ring then spans
     // only up to LAG(KB-1).
     static constexpr int LMAX = KB >= 2 ? LAG(KB - 1) : LAG(KB);
     static constexpr int R = LMAX + 1;
