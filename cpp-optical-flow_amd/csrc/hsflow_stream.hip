@@ -180,9 +180,10 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
     const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
                                                          plane_bytes, 0x00020000);
 
-    // operator rows of step s's stages (issued first in the step: the LDS
-    // latency overlaps the set-up and the horizontal sums)
+    // operator rows of step s's stages (K3_LATE_OPS: each read just before
+    // its stage; else all issued first in the step)
     f2v Xk[KPW], Yk[KPW], Tk[KPW];
+#if !K3_LATE_OPS
     auto fetch_ops = [&](int s1) {
         const int rb = s1 % R;
 #pragma unroll
@@ -200,6 +201,7 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
             }
         }
     };
+#endif
 
     for (int sb = 0; sb < nsteps; sb += P) {
 #pragma unroll
