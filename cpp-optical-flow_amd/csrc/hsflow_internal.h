@@ -21,6 +21,8 @@ struct JacobiArgs {
                                // iterations (memory only), 2 = no memory
                                // traffic (descriptors of size 0)
     int seg_rows;              // K3: output rows per segment (launcher)
+    int band_w;                // K2 workgroup kernel: tile-column band width
+                               // of the tile order (0 = row-major; launcher)
 };
 
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,

@@ -402,7 +402,21 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     const int pair = logical / gridDim.x;
     const int tile = logical - pair * gridDim.x;
     if (tile >= p.tiles_x * p.tiles_y) return;  // whole workgroup: uniform
-    const int ty = tile / p.tiles_x, tx = tile - ty * p.tiles_x;
+    // Tile order inside a pair: row-major, or (band_w > 0) bands of band_w
+    // tile columns walked row-major one band after the other, so that a
+    // tile's upper neighbour was loaded band_w (not tiles_x) workgroups
+    // earlier and its halo rows are still in the XCD's L2.
+    int ty, tx;
+    if (p.band_w > 0 && p.band_w < p.tiles_x) {
+        const int band_tiles = p.band_w * p.tiles_y;
+        const int band = tile / band_tiles, in = tile - band * band_tiles;
+        const int bw = min(p.band_w, p.tiles_x - band * p.band_w);
+        ty = in / bw;
+        tx = band * p.band_w + (in - ty * bw);
+    } else {
+        ty = tile / p.tiles_x;
+        tx = tile - ty * p.tiles_x;
+    }
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int cols = p.cols;
@@ -880,6 +894,12 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     a.tiles_y = (a.rows + OY - 1) / OY;
     const long ntiles = (long)a.tiles_x * a.tiles_y;
     dim3 grd((unsigned)ntiles, (unsigned)a.batch, 1);
+    // tile order: HSFLOW_K2_BAND = band width in tiles (0: row-major)
+    static const int band_env = [] {
+        const char *e = getenv("HSFLOW_K2_BAND");
+        return e ? atoi(e) : 0;
+    }();
+    a.band_w = band_env;
     // diagnostics: HSFLOW_EXTRA_LDS bytes of unused dynamic LDS per workgroup
     // (lowers the workgroups per CU; used to measure occupancy sensitivity)
     static const unsigned extra_lds = [] {
