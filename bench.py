@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=0,
                     help="Jacobi iterations of the CPU sample (0: auto ~15 s)")
     ap.add_argument("--roofline-reps", type=int, default=3)
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time eager solves instead of hipGraph replays of one solve")
     ap.add_argument("--mode", choices=["resident", "stream", "bands"], default="resident",
                     help="resident: pairs generated on each rank, already in HBM "
                          "(the metric); stream: BASELINE config 4, rank 0 holds "
@@ -123,12 +125,40 @@ def main():
                        dtype=torch.uint8, device=dev) if levels > 1 else None)
     stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def solve(s):
         if levels > 1:
             hsflow.flow_pyramid_device(I0, I1, levels, args.window, iters, args.alpha, u, v,
-                                       pws, stream)
+                                       pws, s)
         else:
-            hsflow.flow_device(I0, I1, args.window, iters, args.alpha, u, v, ws, stream)
+            hsflow.flow_device(I0, I1, args.window, iters, args.alpha, u, v, ws, s)
+
+    # A step is one full solve.  By default it is captured once into a
+    # hipGraph (the *_device entry points are stream-ordered and never
+    # synchronise or allocate; tests/test_gpu_parity.py checks replay ==
+    # eager bit for bit) and replayed, so the host does not have to enqueue
+    # the ~100 launches/events of a solve while the GPU waits.
+    graph = None
+    if not args.no_graph:
+        try:
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(stream)
+            with torch.cuda.stream(cap):
+                solve(cap)  # eager once: the library's side streams exist before capture
+            stream.wait_stream(cap)
+            torch.cuda.synchronize(dev)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                solve(torch.cuda.current_stream(dev))
+            torch.cuda.synchronize(dev)
+        except Exception as e:  # pragma: no cover - eager fallback, reported
+            print(f"bench: graph capture failed ({e}); timing eager solves", file=sys.stderr)
+            graph = None
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            solve(stream)
 
     for _ in range(args.warmup):
         step()
@@ -223,7 +253,9 @@ def main():
                        "rows": rows, "cols": cols, "iters": iters, "window": args.window,
                        "levels": levels, "input_dtype": in_dtype,
                        "alpha": args.alpha, "pairs_per_gpu_per_step": batch,
-                       "iters_per_launch": kb, "parallelism": f"frame-parallel x{world}"},
+                       "iters_per_launch": kb, "parallelism": f"frame-parallel x{world}",
+                       "step": "hipGraph replay of one solve" if graph is not None
+                               else "eager solve"},
             "pairs_per_s": round(total_pairs / elapsed, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
