@@ -89,15 +89,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    # HSFLOW_BENCH_BACKEND=gloo + HSFLOW_BENCH_DEVICE=0: rehearse the N > 1
+    # logic with several ranks on one GPU (diagnostics; the driver's runs
+    # use RCCL, one GPU per rank)
+    backend = os.environ.get("HSFLOW_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", int(os.environ.get("HSFLOW_BENCH_DEVICE", local)))
     torch.cuda.set_device(dev)
 
+    def init_dist():
+        if world > 1:
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group(backend)
+
     if args.mode == "stream":
+        init_dist()
         return stream_mode(args, world, rank, dev)
     if args.mode == "bands":
+        init_dist()
         return bands_mode(args, world, rank, dev)
 
     wl = dict(WORKLOADS[args.workload])
@@ -159,6 +169,10 @@ def main():
             graph.replay()
         else:
             solve(stream)
+
+    # the process group comes up after the capture: no communicator thread
+    # touches the device while a stream is capturing
+    init_dist()
 
     for _ in range(args.warmup):
         step()
