@@ -370,12 +370,32 @@ constexpr int wg_rows_tl(int W) {
     return (W == 3 || W == 4 || W == 5) ? 11 : (W == 6 ? 10 : 0);
 }
 
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32, bool ROWE,
+          int PAR>
+__device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
+                                          float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
+                                          float2 *tpl, int tx, int ty, int wv, int lane,
+                                          size_t pbase, int plane_bytes);
+
+// One wave's slab, specialised on the parity of its first image row (the
+// order of the vertical sums follows image-row parity, see wg_body_p): a
+// whole body per parity, so no register state lives across the two.
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32,
           bool ROWE = true>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64], float2 *tpl,
                                         int tx, int ty, int wv, int lane, size_t pbase,
-                                        int plane_bytes);
+                                        int plane_bytes) {
+    constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
+    constexpr int OY = NW * RW - KB * A - KB * AR;
+    const int r0 = ty * OY - KB * A + wv * RW;
+    if ((W == 3 || W == 5) && (r0 & 1))
+        wg_body_p<W, KB, RW, NW, SB, EDGE, X2, G32, ROWE, 1>(p, xch, tpl, tx, ty, wv, lane, pbase,
+                                                            plane_bytes);
+    else
+        wg_body_p<W, KB, RW, NW, SB, EDGE, X2, G32, ROWE, 0>(p, xch, tpl, tx, ty, wv, lane, pbase,
+                                                            plane_bytes);
+}
 
 // 4 waves per SIMD (<= 128 VGPRs): two 8-wave workgroups per CU
 template <int W, int KB, int RW, int NW, int SB>
@@ -461,11 +481,16 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     }
 }
 
-template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32, bool ROWE>
-__device__ __forceinline__ void wg_body(const JacobiArgs &p,
-                                        float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64], float2 *tpl,
-                                        int tx, int ty, int wv, int lane, size_t pbase,
-                                        int plane_bytes) {
+template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32, bool ROWE,
+          int PAR>
+__device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
+                                          float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
+                                          float2 *tpl, int tx, int ty, int wv, int lane,
+                                          size_t pbase, int plane_bytes) {
+    // distinct markers at both ends keep the compiler from hoisting or
+    // sinking the two parity bodies' identical load and store code into the
+    // shared path (which costs ~50 spilled VGPRs at 11-row slabs)
+    asm volatile("; slab parity %0 begin" ::"n"(PAR));
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
     constexpr int HL = KB * A, HR = KB * AR;
     constexpr int HLc = HL + (HL & 1), HRc = HR + (HR & 1);
@@ -591,6 +616,14 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
     };
 
     const int n_it = p.ablate == 1 ? 0 : p.iters;
+    // The vertical sums follow the parity of the image row (PAR = parity
+    // of slab row 0), so every slab height, blocking depth and kernel
+    // adds in the same order.  w = 5: pair sums Q(t) = h(t) + h(t+1) at
+    // odd rows t, cores M(y) = Q(y-1) + Q(y+1) at even rows y, shared by
+    // two outputs: S(y) = h(y-2) + M(y), S(y+1) = M(y) + h(y+3).
+    // w = 3: Q at even rows, S(y) = h(y-1) + Q(y), S(y+1) = Q(y) + h(y+2).
+    // 2 (w = 5) and 1.5 (w = 3) adds per row and field instead of 3 and 2.
+    constexpr bool SHARED = W == 3 || W == 5;
     for (int it = 0; it < n_it; ++it) {
         const int par = wg_nbuf(W, RW) == 2 ? (it & 1) : 0;
         // 1. horizontal sums of the boundary rows first, published for the
@@ -621,7 +654,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
         // those rows are re-zeroed every iteration (EDGE).  So the reads are
         // unconditional, from a clamped slab (no branches, no zero fill).
         const int wa = wv > 0 ? wv - 1 : 0, wb = wv < NW - 1 ? wv + 1 : NW - 1;
-        f2v hu[W], hv[W], qu[W], qv[W];
+        f2v hu[W], hv[W], qu[W], qv[W], mu, mv;
 #pragma unroll
         for (int rr = 0; rr < RW + NB; ++rr) {
             const int t = rr - A;
@@ -645,22 +678,44 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
             } else {
                 hrow(t, hu[sl], hv[sl]);
             }
-            if (rr >= 1) {
+            // pair sum Q(t-1) (w = 5: t-1 odd; w = 3: t-1 even; else every row)
+            if (rr >= 1 && (!SHARED || ((PAR + t - 1 + 2 * W) & 1) == (W == 5 ? 1 : 0))) {
                 const int sp = (t - 1 + 2 * W) % W;
                 qu[sp] = hu[sp] + hu[sl];
                 qv[sp] = hv[sp] + hv[sl];
             }
             const int y = t - AR;  // slab row whose window ends at t
             if (y >= 0) {
-                // pair tree over rows y-A .. y+AR:
-                // ((q(y-A) + q(y-A+2)) + ...) [+ h(y+AR) for odd W], e.g.
-                // w = 5: (q(y-2) + q(y)) + h(y+2);  w = 3: q(y-1) + h(y+1)
+                // other windows: pair tree over rows y-A .. y+AR,
+                // ((q(y-A) + q(y-A+2)) + ...) [+ h(y+AR) for odd W]
                 f2v su, sv;
-                if constexpr (W == 5) {  // the tree below, written out
-                    const int s0 = (y - 2 + 2 * W) % W, s1 = (y + 2 * W) % W,
-                              s2 = (y + 2 + 2 * W) % W;
-                    su = (qu[s0] + qu[s1]) + hu[s2];
-                    sv = (qv[s0] + qv[s1]) + hv[s2];
+                const bool yev = ((PAR + y + 2 * W) & 1) == 0;  // image row y even
+                if constexpr (W == 5) {
+                    const int s0 = (y - 2 + 2 * W) % W, s1 = (y - 1 + 2 * W) % W,
+                              s2 = (y + 1 + 2 * W) % W, s3 = (y + 2 + 2 * W) % W;
+                    if (yev) {  // S(y) = h(y-2) + (Q(y-1) + Q(y+1))
+                        mu = qu[s1] + qu[s2];
+                        mv = qv[s1] + qv[s2];
+                        su = hu[s0] + mu;
+                        sv = hv[s0] + mv;
+                    } else {  // S(y) = (Q(y-2) + Q(y)) + h(y+2)
+                        if (y == 0) {  // core M(-1) not formed by row -1
+                            mu = qu[s0] + qu[(y + 2 * W) % W];
+                            mv = qv[s0] + qv[(y + 2 * W) % W];
+                        }
+                        su = mu + hu[s3];
+                        sv = mv + hv[s3];
+                    }
+                } else if constexpr (W == 3) {
+                    const int s0 = (y - 1 + 2 * W) % W, s1 = (y + 2 * W) % W,
+                              s2 = (y + 1 + 2 * W) % W;
+                    if (yev) {  // S(y) = h(y-1) + Q(y)
+                        su = hu[s0] + qu[s1];
+                        sv = hv[s0] + qv[s1];
+                    } else {  // S(y) = Q(y-1) + h(y+1)
+                        su = qu[s0] + hu[s2];
+                        sv = qv[s0] + hv[s2];
+                    }
                 } else {
                     su = qu[(y - A + 2 * W) % W];
                     sv = qv[(y - A + 2 * W) % W];
@@ -712,6 +767,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
         if constexpr (wg_nbuf(W, RW) == 1) __syncthreads();
     }
 
+    asm volatile("; slab parity %0 sweep end" ::"n"(PAR));
     // interior tile: workgroup rows [HL, HL + OY), lanes [HLc/2, (HLc + OX)/2)
     const auto uo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_out + pbase), 0,
                                                          nbytes, 0x00020000);
@@ -738,6 +794,7 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, oo, 0, 0);
         }
     }
+    asm volatile("; slab parity %0 end" ::"n"(PAR));
 }
 
 // ---------------------------------------------------------------------- K2g

@@ -122,10 +122,10 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
 
     // rings of horizontal sums and vertical pair sums, per local stage, and
     // each stage's last output row (the next stage's input one step later)
-    f2v hu[KPW][W], hv[KPW][W], qu[KPW][W], qv[KPW][W], ou[KPW], ov[KPW];
+    f2v hu[KPW][W], hv[KPW][W], qu[KPW][W], qv[KPW][W], ou[KPW], ov[KPW], mu[KPW], mv[KPW];
 #pragma unroll
     for (int i = 0; i < KPW; ++i) {
-        ou[i] = ov[i] = f2v{0.f, 0.f};
+        ou[i] = ov[i] = mu[i] = mv[i] = f2v{0.f, 0.f};
 #pragma unroll
         for (int w = 0; w < W; ++w) hu[i][w] = hv[i][w] = qu[i][w] = qv[i][w] = f2v{0.f, 0.f};
     }
@@ -267,17 +267,44 @@ __device__ __forceinline__ void k3_role(const JacobiArgs &p, K3Lds<W, KB, S> &L,
                     hu[i][sl] = f2v{a, b};
                     hv[i][sl] = f2v{c, d};
                 }
-                qu[i][sp] = hu[i][sp] + hu[i][sl];
-                qv[i][sp] = hv[i][sp] + hv[i][sl];
-                // output row y = t - AR: pair tree over rows y-A .. y+AR
+                // Relative row r equals image row r0 + r with r0 even
+                // (launch_k3), so the vertical sums follow image-row parity
+                // exactly as in K2 (hsflow_kernels.hip, wg_body_p): w = 5
+                // pair sums at odd rows and shared cores at even rows, w = 3
+                // pair sums at even rows.  sb is a multiple of the even P.
+                const int tph = ph - G::D(k);  // input row, relative to sb
+                if ((W != 3 && W != 5) || k3_mod(tph - 1, 2) == (W == 5 ? 1 : 0)) {
+                    qu[i][sp] = hu[i][sp] + hu[i][sl];
+                    qv[i][sp] = hv[i][sp] + hv[i][sl];
+                }
+                // output row y = t - AR
                 const int yph = ph - G::LAG(k);
+                const bool yev = k3_mod(yph, 2) == 0;
                 f2v su, sv;
                 if constexpr (W == 5) {
-                    const int s0 = k3_mod(yph - 2, W), s1 = k3_mod(yph, W),
-                              s2 = k3_mod(yph + 2, W);
-                    su = (qu[i][s0] + qu[i][s1]) + hu[i][s2];
-                    sv = (qv[i][s0] + qv[i][s1]) + hv[i][s2];
+                    const int s0 = k3_mod(yph - 2, W), s1 = k3_mod(yph - 1, W),
+                              s2 = k3_mod(yph + 1, W), s3 = k3_mod(yph + 2, W);
+                    if (yev) {  // S(y) = h(y-2) + (Q(y-1) + Q(y+1))
+                        mu[i] = qu[i][s1] + qu[i][s2];
+                        mv[i] = qv[i][s1] + qv[i][s2];
+                        su = hu[i][s0] + mu[i];
+                        sv = hv[i][s0] + mv[i];
+                    } else {  // S(y) = (Q(y-2) + Q(y)) + h(y+2), core of row y-1
+                        su = mu[i] + hu[i][s3];
+                        sv = mv[i] + hv[i][s3];
+                    }
+                } else if constexpr (W == 3) {
+                    const int s0 = k3_mod(yph - 1, W), s1 = k3_mod(yph, W),
+                              s2 = k3_mod(yph + 1, W);
+                    if (yev) {  // S(y) = h(y-1) + Q(y)
+                        su = hu[i][s0] + qu[i][s1];
+                        sv = hv[i][s0] + qv[i][s1];
+                    } else {  // S(y) = Q(y-1) + h(y+1)
+                        su = qu[i][s0] + hu[i][s2];
+                        sv = qv[i][s0] + hv[i][s2];
+                    }
                 } else {
+                    // other windows: pair tree over rows y-A .. y+AR
                     su = qu[i][k3_mod(yph - A, W)];
                     sv = qv[i][k3_mod(yph - A, W)];
 #pragma unroll
@@ -437,6 +464,10 @@ static hipError_t launch_k3(JacobiArgs a, hipStream_t s) {
         seg = (int)((a.rows + nseg - 1) / nseg);
         if (seg < 32) seg = 32;
     }
+    // even segment starts: with an even A * KB every relative row has the
+    // parity of its image row (the vertical summation order depends on it)
+    static_assert((G::A * KB) % 2 == 0, "relative rows keep image-row parity");
+    seg += seg & 1;
     a.seg_rows = seg;
     a.tiles_y = (a.rows + seg - 1) / seg;
     const long nwg = (long)a.tiles_x * a.tiles_y * a.batch;

@@ -77,7 +77,11 @@ def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk: int)
     A, AR = anchors(window)
     H = chunk * max(A, AR, 1)
     H += H & 1                      # even: extended bands start on even rows
-    align = 1 << (levels - 1)       # nested bands on every level
+    # nested bands on every level, each starting on an even row (even at the
+    # coarsest level): the Jacobi kernels add the vertical window sums in an
+    # order fixed by image-row parity, so a band solved as its own plane
+    # must keep that parity to stay bit-identical to the whole-frame solve
+    align = 1 << levels
     sizes = [(rows, cols)]
     for _ in range(1, levels):
         r, c = sizes[-1]

@@ -68,8 +68,9 @@ def test_plan_bands_tile_and_nest(rows, levels, world, chunk):
             assert bd.b - bd.a >= p.halo or world == 1
             assert bd.e0 == (0 if k == 0 else bd.a - p.halo)
             assert bd.e1 == (R if k == world - 1 else bd.b + p.halo)
-            if l < levels - 1:                              # levels warm-started from
-                assert bd.e0 % 2 == 0                       # a coarser one map rows exactly
+            # even band starts: warm starts map rows exactly and the band keeps
+            # image-row parity (the kernels' vertical summation order)
+            assert bd.e0 % 2 == 0
             if l > 0:
                 assert bd.a == p.bands[0][k].a >> l         # bands nest across levels
 
