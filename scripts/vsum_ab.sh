@@ -1,5 +1,6 @@
 # Parity of the in-tree build (blocking-depth invariance, oracle), then a
-# same-box A/B of two library builds x slab settings.
+# same-box A/B of two library builds x slab settings.  abx/old.so and
+# abx/new2.so are built ad hoc (make, then copy) and not kept in the tree.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread \
