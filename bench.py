@@ -6,20 +6,35 @@ One step = one full solve (K1 gradients + `iters` Jacobi iterations, the
 reference's getFlow, hornSchunck.cpp:43-75) of a batch of synthetic frame
 pairs per GPU, inputs already resident in HBM (workload 8k = BASELINE config
 5: an fp16 7680x4320 pair through the 3-level coarse-to-fine warm start,
-`iters` per level; its Mpix*iter counts every level's pixels).  Frame pairs are independent,
-so for N > 1 each rank (one process per GPU, torch.distributed over RCCL)
-solves its own pairs: weak scaling, no data-path collective (the timing
-barrier and max-over-ranks reduction are the only collectives).
+`iters` per level; its Mpix*iter counts every level's pixels).  Frame pairs
+are independent, so for N > 1 each rank (one process per GPU,
+torch.distributed over RCCL) solves its own pairs: weak scaling, no
+data-path collective (the timing barrier and max-over-ranks reduction are
+the only collectives in the headline leg).
 
 Rank 0 prints ONE JSON line.  Besides the driver fields it carries
+  parity        pair 0 of the TIMED solve (seed 1000) against the float64
+                oracle's golden checksums (tests/golden/bench_golden.*,
+                made by tests/golden/make_bench_golden.py): max|du|/max|u| on
+                a strided sample and the whole-plane sums.  A mismatch exits
+                non-zero; so does a probe build of the library or any
+                HSFLOW_* diagnostic variable in the environment.
   roofline      dominant kernel (K2, hs_jacobi_wg_kernel) measured live with
-                events on the launch stream; achieved = SURVEY §8(d)'s 28 B
+                events on its launch stream; achieved = SURVEY §8(d)'s 28 B
                 per pixel-iteration x the pixel-iterations of one launch /
                 launch time (> peak is possible: temporal blocking does KB
-                iterations per HBM pass); compulsory_* = the 20 B/px one
-                blocked pass must move, which PMC `traffic` (committed
-                rocprofv3 summary under profiles/, or null) is compared with
+                iterations per HBM pass); hbm_frac = PMC bytes per launch
+                (committed profile) / launch time / 8 TB/s; valu_frac = VALU
+                issue cycles / launch cycles from the same profile
                 (DESIGN.md "Roofline")
+  secondary     the default run also times BASELINE configs[2] (4K x 500 it)
+                with its own roofline and parity check
+  pairs_per_s_resident / pairs_per_s_e2e
+                pairs/s with inputs in HBM, and end to end as BASELINE.md
+                defines it: pinned host u8 frames -> H2D -> K1 + K2 -> D2H
+                of (u, v) f32, copies overlapped with solves on other streams
+  stream        BASELINE config 4: 64 pairs held by rank 0, scattered over
+                RCCL (point-to-point), solved, (u, v) gathered back
   cpu_baseline  the float64 CPU port (oracle/, mirrors hornSchunck.cpp pass
                 by pass) on a bounded sample, 1 thread, rank 0 only
 """
@@ -38,14 +53,24 @@ WORKLOADS = {
     # BASELINE.json configs[1] / configs[2]
     "1080p": dict(rows=1080, cols=1920, iters=300, batch=8),
     "4k": dict(rows=2160, cols=3840, iters=500, batch=2),
-    # BASELINE.json configs[4] on one GPU (the 8-GPU row-band split is not a
-    # bench line; frame-parallel weak scaling is)
+    # BASELINE.json configs[4] on one GPU (the 8-GPU row-band split is
+    # --mode bands; frame-parallel weak scaling is the headline)
     "8k": dict(rows=4320, cols=7680, iters=1000, batch=1, levels=3, dtype="f16"),
 }
-HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+VALU_ISSUE_CYCLES = 4.0    # wave64 VALU / v_pk_*_f32 issue cost per SIMD,
+                           # measured in shader cycles (scripts/ubench/valu_tput.hip,
+                           # profiles/r02_valu_tput.txt)
+SIMDS = 1024               # 256 CUs x 4
+PARITY_TOL = 1e-4          # north_star: 1e-4 relative (norm form)
+GOLDEN_JSON = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
+GOLDEN_NPZ = os.path.join(ROOT, "tests", "golden", "bench_golden.npz")
+# HSFLOW_* variables the bench itself reads (rehearsal of the N > 1 logic
+# with several ranks on one GPU); every other HSFLOW_* name is refused
+BENCH_ENV = {"HSFLOW_BENCH_BACKEND", "HSFLOW_BENCH_DEVICE"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -67,57 +92,123 @@ def parse():
     ap.add_argument("--roofline-reps", type=int, default=3)
     ap.add_argument("--no-graph", action="store_true",
                     help="time eager solves instead of hipGraph replays of one solve")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the configs[2] (4K) block of the default run")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pairs/s leg")
+    ap.add_argument("--no-stream", action="store_true", help="skip the config-4 stream leg")
     ap.add_argument("--mode", choices=["resident", "stream", "bands"], default="resident",
                     help="resident: pairs generated on each rank, already in HBM "
-                         "(the metric); stream: BASELINE config 4, rank 0 holds "
-                         "--pairs pairs and scatters/gathers them over RCCL; bands: "
-                         "BASELINE config 5 on N GPUs, ONE pair split into row bands "
-                         "with a halo exchange (row_bands.py)")
+                         "(the metric, plus the secondary / e2e / stream legs); stream: "
+                         "BASELINE config 4 alone; bands: BASELINE config 5 on N GPUs, "
+                         "ONE pair split into row bands with a halo exchange")
     ap.add_argument("--chunk", type=int, default=12,
                     help="bands mode: iterations between halo exchanges")
-    ap.add_argument("--pairs", type=int, default=64, help="stream mode: pairs in the stream")
-    return ap.parse_args()
+    ap.add_argument("--pairs", type=int, default=64, help="stream leg: pairs in the stream")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+# --------------------------------------------------------------- guards
+def refuse_diagnostics(environ=None):
+    """Names of HSFLOW_* variables that could change the measured work
+    (diagnostic switches live only in the probe build, but the bench refuses
+    them outright so a stray variable can never produce a number)."""
+    environ = os.environ if environ is None else environ
+    return sorted(k for k in environ if k.startswith("HSFLOW_") and k not in BENCH_ENV)
+
+
+# --------------------------------------------------------------- parity
+def golden_entry(rows, cols, iters, window, levels, alpha):
+    """(name, meta, u_sample, v_sample) of the committed oracle golden for
+    this configuration, or None."""
     import numpy as np
+    if not (os.path.exists(GOLDEN_JSON) and os.path.exists(GOLDEN_NPZ)):
+        return None
+    meta = json.load(open(GOLDEN_JSON))
+    for name, e in meta.items():
+        if (e["rows"], e["cols"], e["iters"], e["window"], e["levels"], e["alpha"]) == \
+                (rows, cols, iters, window, levels, alpha):
+            z = np.load(GOLDEN_NPZ)
+            return name, e, z[name + "_u"], z[name + "_v"]
+    return None
+
+
+def parity_check(u, v, golden):
+    """u, v: full float planes (numpy) of pair seed 1000.  Compares the
+    strided sample elementwise (max|d| / max|ref|, the SURVEY §8c form, scale
+    = the oracle's full-plane max) and the plane sums (|dSum| / (n max|ref|))."""
+    import numpy as np
+    if golden is None:
+        return {"ok": None, "reason": "no golden for this configuration"}
+    name, e, us, vs = golden
+    step = e["step"]
+    n = u.size
+    out = {"golden": name, "tol": PARITY_TOL}
+    errs, sums = [], []
+    for got, ref, s_ref, m_ref in ((u, us, e["sum_u"], e["max_u"]),
+                                   (v, vs, e["sum_v"], e["max_v"])):
+        g = np.asarray(got, np.float64)
+        errs.append(float(np.max(np.abs(g[::step, ::step] - ref))) / m_ref)
+        sums.append(abs(float(g.sum()) - s_ref) / (n * m_ref))
+    out["max_rel_err"] = max(errs)
+    out["sum_rel_err"] = max(sums)
+    out["ok"] = bool(np.isfinite(u).all() and np.isfinite(v).all() and
+                     out["max_rel_err"] <= PARITY_TOL and out["sum_rel_err"] <= PARITY_TOL)
+    return out
+
+
+# --------------------------------------------------------------- timing
+def timed_region(step, sync, steps, warmup, world, device):
+    """The driver's timing rule: W untimed steps, barrier + sync, K timed
+    steps, sync; the slowest rank's time."""
     import torch
     import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    return elapsed
+
+
+def pmc_for(workload, kb, batch):
+    """Committed PMC summary (profiles/pmc_<workload>.json) if it was
+    collected for this blocking depth and batch."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    if pmc.get("kb") == kb and pmc.get("batch") == batch:
+        return pmc
+    return None
+
+
+# --------------------------------------------------------------- resident
+def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False):
+    """One workload, inputs resident in HBM: a step is one full solve of
+    `batch` pairs per rank (hipGraph replay).  Returns the leg's dict."""
+    import numpy as np
+    import torch
     import hsflow
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # HSFLOW_BENCH_BACKEND=gloo + HSFLOW_BENCH_DEVICE=0: rehearse the N > 1
-    # logic with several ranks on one GPU (diagnostics; the driver's runs
-    # use RCCL, one GPU per rank)
-    backend = os.environ.get("HSFLOW_BENCH_BACKEND", "nccl")
-    dev = torch.device("cuda", int(os.environ.get("HSFLOW_BENCH_DEVICE", local)))
-    torch.cuda.set_device(dev)
-
-    def init_dist():
-        if world > 1:
-            if backend == "nccl":
-                dist.init_process_group("nccl", device_id=dev)
-            else:
-                dist.init_process_group(backend)
-
-    if args.mode == "stream":
-        init_dist()
-        return stream_mode(args, world, rank, dev)
-    if args.mode == "bands":
-        init_dist()
-        return bands_mode(args, world, rank, dev)
-
-    wl = dict(WORKLOADS[args.workload])
+    wl = dict(WORKLOADS[wl_name])
     rows, cols = wl["rows"], wl["cols"]
     iters = args.iters or wl["iters"]
     batch = args.batch or wl["batch"]
     levels = args.levels or wl.get("levels", 1)
     in_dtype = args.dtype or wl.get("dtype", "f32")
-    if args.kb:
-        hsflow.set_iters_per_launch(args.kb)
+    window, alpha = args.window, args.alpha
 
     # synthetic pairs, seed 1000 + global pair index (SURVEY §8d)
     np_dtype = np.uint8 if in_dtype == "u8" else np.float32
@@ -137,16 +228,13 @@ def main():
 
     def solve(s):
         if levels > 1:
-            hsflow.flow_pyramid_device(I0, I1, levels, args.window, iters, args.alpha, u, v,
-                                       pws, s)
+            hsflow.flow_pyramid_device(I0, I1, levels, window, iters, alpha, u, v, pws, s)
         else:
-            hsflow.flow_device(I0, I1, args.window, iters, args.alpha, u, v, ws, s)
+            hsflow.flow_device(I0, I1, window, iters, alpha, u, v, ws, s)
 
-    # A step is one full solve.  By default it is captured once into a
-    # hipGraph (the *_device entry points are stream-ordered and never
-    # synchronise or allocate; tests/test_gpu_parity.py checks replay ==
-    # eager bit for bit) and replayed, so the host does not have to enqueue
-    # the ~100 launches/events of a solve while the GPU waits.
+    # A step is one full solve, captured once into a hipGraph and replayed
+    # (the *_device entry points are stream-ordered and never synchronise or
+    # allocate; tests/test_gpu_parity.py checks replay == eager bit for bit).
     graph = None
     if not args.no_graph:
         try:
@@ -170,192 +258,337 @@ def main():
         else:
             solve(stream)
 
-    # the process group comes up after the capture: no communicator thread
-    # touches the device while a stream is capturing
-    init_dist()
+    # the process group comes up after the first capture: no communicator
+    # thread touches the device while a stream is capturing
+    if init_dist is not None:
+        init_dist()
+    elapsed = timed_region(step, lambda: torch.cuda.synchronize(dev), args.steps,
+                           args.warmup, world, dev)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
+    # parity of the timed output: pair 0 of rank 0 is seed 1000
+    parity = None
+    if rank == 0:
+        golden = golden_entry(rows, cols, iters, window, levels, alpha)
+        parity = parity_check(u[0].cpu().numpy(), v[0].cpu().numpy(), golden)
 
-    px = rows * cols
-    # pixels swept per iteration, summed over the pyramid levels
     px_all = sum(r * c for r, c in (hsflow.pyramid_level_size(rows, cols, l)
                                     for l in range(levels)))
     total_pairs = batch * world * args.steps
     value = total_pairs * px_all * iters / elapsed / 1e6
-    ok = bool(torch.isfinite(u).all().item()) and 0.05 < float(u.mean()) < 0.3
 
-    # ---- dominant-kernel roofline: K2 alone, events on the launch stream --
-    kb = hsflow.iters_per_launch(rows, cols, batch, args.window) if not args.kb else args.kb
+    # ---- dominant-kernel roofline: K2 alone, events on its launch stream
+    kb = hsflow.iters_per_launch(rows, cols, batch, window)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    hsflow.gradients_device(I0, I1, ws, stream=stream)
+    # (config 5: K2 on the level-0 plane, the pass that dominates the solve)
+    rws = ws if levels == 1 else hsflow.alloc_workspace(rows, cols, batch, dev)
+    hsflow.gradients_device(I0, I1, rws, stream=stream)
     launches_per_solve = -(-iters // kb)
     reps = args.roofline_reps
-    # one stream here so the per-launch duration is what rocprofv3 reports
-    # per dispatch (the batch split overlaps launches and would blur it)
+    # one stream so the per-launch duration is what rocprofv3 reports per
+    # dispatch (the batch split overlaps launches and would blur it)
     hsflow.set_max_streams(1)
     torch.cuda.synchronize(dev)
     ev0.record(stream)
     for _ in range(reps):
-        hsflow.jacobi_device(rows, cols, batch, args.window, iters, args.alpha, u, v, ws,
+        hsflow.jacobi_device(rows, cols, batch, window, iters, alpha, u, v, rws,
                              stream=stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     hsflow.set_max_streams(0)
     k2_ms = ev0.elapsed_time(ev1) / (reps * launches_per_solve)
-    n_px = batch * px
+    n_px = batch * rows * cols
     # algorithmic bytes = 28 B per pixel-iteration (read u, v,
     # Ix, Iy, It; write u', v' in f32) x the pixel-iterations one launch
     # performs -- fixed by the algorithm, whatever the blocking saves
-    px_iters_per_launch = n_px * iters / launches_per_solve
-    bytes_per_launch = 28.0 * px_iters_per_launch
+    bytes_per_launch = 28.0 * n_px * iters / launches_per_solve
     achieved = bytes_per_launch / (k2_ms * 1e-3) / 1e9
-    # the HBM bytes one temporally-blocked pass cannot avoid (what the PMC
-    # traffic is compared with): read u, v (f32) + packed gradients (4 B),
-    # write u, v; the first pass of a solve reads no u, v
-    first_frac = 1.0 / launches_per_solve
-    compulsory = n_px * (8 + 4 + 8 - 8 * first_frac)
+    # the HBM bytes one temporally-blocked pass cannot avoid: read u, v (f32)
+    # + packed gradients (4 B), write u, v; the first pass reads no u, v
+    compulsory = n_px * (8 + 4 + 8 - 8 / launches_per_solve)
     compulsory_gbps = compulsory / (k2_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": "hs_jacobi_wg_kernel", "avg_launch_ms": round(k2_ms, 5),
+            "iters_per_launch": kb, "launches_per_solve": launches_per_solve,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "algorithmic_B_per_px_iter": 28,
+            "compulsory_bytes_per_launch": int(compulsory),
+            "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4),
+            "hbm_frac": None, "valu_frac": None}
+    pmc = pmc_for(wl_name, kb, batch) if levels == 1 and window == 5 else None
+    if pmc is not None:
+        traffic = pmc["hbm_bytes_per_launch"]
+        roof["traffic"] = traffic
+        # physical HBM utilisation: the PMC bytes at the live launch time
+        roof["hbm_frac"] = round(traffic / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        if pmc.get("valu_insts_per_launch") and pmc.get("launch_cycles"):
+            # VALU issue cycles per SIMD / the launch's shader cycles (both
+            # from the profile; GRBM_GUI_ACTIVE / 8 XCDs = launch cycles)
+            roof["valu_frac"] = round(pmc["valu_insts_per_launch"] * VALU_ISSUE_CYCLES /
+                                      SIMDS / pmc["launch_cycles"], 4)
+            roof["clock_ghz"] = pmc.get("clock_ghz")
+        roof["pmc_source"] = pmc.get("source")
 
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        if pmc.get("kb") == kb and pmc.get("batch") == batch:
-            traffic = pmc.get("hbm_bytes_per_launch")
-
-    cpu = cpu_all = None
-    if rank == 0 and not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(rows, cols, args.window, args.alpha, args.cpu_iters)
-        # SURVEY §8(d) second CPU line: all cores of the box's CPU share
-        # (16 per GPU on the MI355X pool; os.cpu_count() shows the machine)
-        n_thr = min(16, os.cpu_count() or 1)
-        cpu_all = cpu_baseline(rows, cols, args.window, args.alpha, args.cpu_iters, n_thr)
-
-    if rank == 0:
-        line = {
-            "metric": "Mpix*iter/s (Horn-Schunck Jacobi) + frame-pairs/s",
-            "value": round(value, 1),
-            "unit": "Mpix*iter/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": f"synthetic {in_dtype} frame pairs (hash texture, shift (-0.75,+1.5) px)",
-            "config": {"workload": f"{args.workload} {cols}x{rows}, {iters} it"
-                                   + (f"/level x {levels} levels" if levels > 1 else "")
-                                   + f", ws {args.window}",
-                       "rows": rows, "cols": cols, "iters": iters, "window": args.window,
-                       "levels": levels, "input_dtype": in_dtype,
-                       "alpha": args.alpha, "pairs_per_gpu_per_step": batch,
-                       "iters_per_launch": kb, "parallelism": f"frame-parallel x{world}",
-                       "step": "hipGraph replay of one solve" if graph is not None
-                               else "eager solve"},
-            "pairs_per_s": round(total_pairs / elapsed, 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
-                         "kernel": "hs_jacobi_wg_kernel",
-                         "avg_launch_ms": round(k2_ms, 5),
-                         "iters_per_launch": kb,
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "algorithmic_B_per_px_iter": 28,
-                         "compulsory_bytes_per_launch": int(compulsory),
-                         "compulsory_GBps": round(compulsory_gbps, 1),
-                         "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4),
-                         # measured (DESIGN.md §4 Roofline): the pass is bound
-                         # by VALU issue, its compute phase at ~95 % of the
-                         # wave64 VALU rate; HBM is the nominal SURVEY class
-                         "limiter": "valu"},
-            "cpu_baseline": cpu,
-            "cpu_baseline_all_cores": cpu_all,
-            "sane": ok,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    leg = {"workload": f"{wl_name} {cols}x{rows}, {iters} it"
+                       + (f"/level x {levels} levels" if levels > 1 else "")
+                       + f", ws {window}",
+           "rows": rows, "cols": cols, "iters": iters, "window": window, "levels": levels,
+           "input_dtype": in_dtype, "alpha": alpha, "pairs_per_gpu_per_step": batch,
+           "value": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "pairs_per_s_resident": round(total_pairs / elapsed, 2),
+           "step": "hipGraph replay of one solve" if graph is not None else "eager solve",
+           "roofline": roof, "parity": parity}
+    del I0, I1, u, v, ws, pws, graph
+    torch.cuda.empty_cache()
+    return leg
 
 
-def stream_mode(args, world, rank, dev):
-    """BASELINE config 4: a stream of --pairs synthetic frame pairs held by
-    rank 0, scattered one-per-rank round-robin over RCCL (point-to-point),
-    solved (each rank batches its share into one hsflow_flow_device call),
-    and (u, v) gathered back to rank 0.  Timed end to end (scatter + solve +
-    gather), max over ranks.  Reported as pairs/s and Mpix*iter/s."""
+# --------------------------------------------------------------- e2e
+def e2e_leg(wl_name, args, dev, n_batches=6):
+    """End-to-end pairs/s as BASELINE.md defines it: pinned host u8 gray
+    frames (what main.cpp:13-14 hands over) -> H2D -> K1 + K2 -> D2H of u, v
+    (f32), batch after batch.  Copies run on their own streams and overlap
+    the neighbouring batches' solves (double-buffered device slots)."""
     import numpy as np
     import torch
-    import torch.distributed as dist
     import hsflow
-    import frame_parallel as fp
 
-    wl = dict(WORKLOADS[args.workload])
+    wl = WORKLOADS[wl_name]
+    rows, cols, iters, batch = wl["rows"], wl["cols"], args.iters or wl["iters"], wl["batch"]
+    host_in = []
+    for k in range(2):  # two distinct host batches, alternating
+        ps = [hsflow.synth_pair(1000 + 8 * k + i, rows, cols, dtype=np.uint8)
+              for i in range(batch)]
+        host_in.append((torch.from_numpy(np.stack([p[0] for p in ps])).pin_memory(),
+                        torch.from_numpy(np.stack([p[1] for p in ps])).pin_memory()))
+    shp = (batch, rows, cols)
+    d_in = [(torch.empty(shp, dtype=torch.uint8, device=dev),
+             torch.empty(shp, dtype=torch.uint8, device=dev)) for _ in range(2)]
+    d_out = [(torch.empty(shp, dtype=torch.float32, device=dev),
+              torch.empty(shp, dtype=torch.float32, device=dev)) for _ in range(2)]
+    h_out = [(torch.empty(shp, dtype=torch.float32).pin_memory(),
+              torch.empty(shp, dtype=torch.float32).pin_memory()) for _ in range(2)]
+    ws = [hsflow.alloc_workspace(rows, cols, batch, dev) for _ in range(2)]
+    s_h2d, s_cmp, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
+    ev = {k: [torch.cuda.Event() for _ in range(2)]
+          for k in ("in", "done", "in_free", "out_free")}
+
+    def run(n):
+        for k in range(n):
+            sl = k % 2
+            a, b = host_in[k % 2]
+            with torch.cuda.stream(s_h2d):
+                if k >= 2:
+                    s_h2d.wait_event(ev["in_free"][sl])
+                d_in[sl][0].copy_(a, non_blocking=True)
+                d_in[sl][1].copy_(b, non_blocking=True)
+                ev["in"][sl].record(s_h2d)
+            with torch.cuda.stream(s_cmp):
+                s_cmp.wait_event(ev["in"][sl])
+                if k >= 2:
+                    s_cmp.wait_event(ev["out_free"][sl])
+                hsflow.flow_device(d_in[sl][0], d_in[sl][1], args.window, iters, args.alpha,
+                                   d_out[sl][0], d_out[sl][1], ws[sl], s_cmp)
+                ev["in_free"][sl].record(s_cmp)
+                ev["done"][sl].record(s_cmp)
+            with torch.cuda.stream(s_d2h):
+                s_d2h.wait_event(ev["done"][sl])
+                h_out[sl][0].copy_(d_out[sl][0], non_blocking=True)
+                h_out[sl][1].copy_(d_out[sl][1], non_blocking=True)
+                ev["out_free"][sl].record(s_d2h)
+        torch.cuda.synchronize(dev)
+
+    run(2)  # warm-up (side streams, allocator)
+    t = time.perf_counter()
+    run(n_batches)
+    dt = time.perf_counter() - t
+    ok = bool(torch.isfinite(h_out[0][0]).all())
+    return {"pairs_per_s_e2e": round(n_batches * batch / dt, 2),
+            "e2e": {"workload": f"{wl_name}, {batch} pairs per batch, {n_batches} batches",
+                    "input": "pinned host u8 gray frames", "output": "pinned host f32 u, v",
+                    "ms_per_batch": round(dt / n_batches * 1e3, 3), "finite": ok}}
+
+
+# --------------------------------------------------------------- stream
+def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
+    """BASELINE config 4: a stream of n_pairs synthetic frame pairs held by
+    rank 0, scattered one-per-rank round-robin (point-to-point over RCCL;
+    gloo in the CPU tests), each rank's share solved in one batched call,
+    (u, v) gathered back to rank 0.  Timed end to end, max over ranks."""
+    import torch
+    import frame_parallel as fp
+    import hsflow
+
+    wl = WORKLOADS[wl_name]
     rows, cols = wl["rows"], wl["cols"]
     iters = args.iters or wl["iters"]
-    n = args.pairs
+    n = n_pairs or args.pairs
     stream = None
     if rank == 0:
         stream = [tuple(torch.from_numpy(a).to(dev) for a in
                         hsflow.synth_pair(1000 + j, rows, cols)) for j in range(n)]
     mine = fp.my_pairs(n, rank, world)
-    ws = hsflow.alloc_workspace(rows, cols, max(1, len(mine)), dev)
+    if solve_batch is None:
+        ws = hsflow.alloc_workspace(rows, cols, max(1, len(mine)), dev)
+
+        def solve_batch(I0, I1):
+            return hsflow.flow_device(I0, I1, args.window, iters, args.alpha, workspace=ws)
+
+    out = [None]
 
     def one_pass():
         pairs = fp.scatter_pairs(stream, n, (rows, cols), torch.float32, dev, rank, world)
         flows = []
         if pairs:
-            I0 = torch.stack([p[0] for p in pairs])
-            I1 = torch.stack([p[1] for p in pairs])
-            u, v = hsflow.flow_device(I0, I1, args.window, iters, args.alpha, workspace=ws)
+            u, v = solve_batch(torch.stack([p[0] for p in pairs]),
+                               torch.stack([p[1] for p in pairs]))
             flows = [(u[k], v[k]) for k in range(len(pairs))]
-        return fp.gather_flows(flows, n, (rows, cols), dev, rank, world)
+        out[0] = fp.gather_flows(flows, n, (rows, cols), dev, rank, world)
 
-    for _ in range(args.warmup):
-        one_pass()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = one_pass()
-    torch.cuda.synchronize(dev)
-    elapsed = fp.max_over_ranks(time.perf_counter() - t0, dev, world)
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    steps = max(1, min(args.steps, 3))
+    elapsed = timed_region(one_pass, sync, steps, 1, world, dev)
+    leg = {"pairs_per_s": round(n * steps / elapsed, 2),
+           "ms_per_pass": round(elapsed / steps * 1e3, 3), "pairs": n,
+           "Mpix_iter_per_s": round(n * steps * rows * cols * iters / elapsed / 1e6, 1),
+           "transport": ("RCCL point-to-point" if world > 1 and dev.type == "cuda"
+                         else ("gloo" if world > 1 else "none (one rank)")),
+           "scaling": "strong"}
     if rank == 0:
-        ok = len(out) == n and all(bool(torch.isfinite(u).all()) for u, _ in out[:2])
-        total = n * args.steps
-        print(json.dumps({
-            "metric": "frame-pairs/s (config 4 stream: RCCL scatter + solve + gather)",
-            "value": round(total / elapsed, 2), "unit": "pairs/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic f32 frame pairs",
-            "config": {"workload": f"stream of {n} x {args.workload} pairs, {iters} it",
-                       "pairs": n, "iters": iters, "window": args.window,
-                       "parallelism": f"frame-parallel x{world}"},
-            "Mpix_iter_per_s": round(total * rows * cols * iters / elapsed / 1e6, 1),
-            "sane": ok}), flush=True)
+        res = out[0]
+        leg["gathered"] = len(res) if res is not None else 0
+        leg["finite"] = bool(res is not None and all(bool(torch.isfinite(u).all())
+                                                      for u, _ in res[:2]))
+    return leg
+
+
+# --------------------------------------------------------------- main
+def main():
+    args = parse()
+    bad = refuse_diagnostics()
+    if bad:
+        print(f"bench: refusing to run with diagnostic variables set: {bad}", file=sys.stderr)
+        sys.exit(2)
+    import torch
+    import torch.distributed as dist
+    import hsflow
+
+    if hsflow.is_probe_build():
+        print(f"bench: {hsflow.LIB_PATH} is the probe build; rebuild the product library",
+              file=sys.stderr)
+        sys.exit(2)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # HSFLOW_BENCH_BACKEND=gloo + HSFLOW_BENCH_DEVICE=0: rehearse the N > 1
+    # logic with several ranks on one GPU (diagnostics; the driver's runs
+    # use RCCL, one GPU per rank)
+    backend = os.environ.get("HSFLOW_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", int(os.environ.get("HSFLOW_BENCH_DEVICE", local)))
+    torch.cuda.set_device(dev)
+
+    state = {"up": False}
+
+    def init_dist():
+        if world > 1 and not state["up"]:
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group(backend)
+            state["up"] = True
+
+    if args.mode == "stream":
+        init_dist()
+        leg = stream_leg(args.workload, args, world, rank, dev)
+        if rank == 0:
+            print(json.dumps({
+                "metric": "frame-pairs/s (config 4 stream: RCCL scatter + solve + gather)",
+                "value": leg["pairs_per_s"], "unit": "pairs/s", "n_gpus": world,
+                "steps": max(1, min(args.steps, 3)), "warmup": 1,
+                "ms_per_step": leg["ms_per_pass"], "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic f32 frame pairs",
+                "config": {"workload": f"stream of {leg['pairs']} x {args.workload} pairs",
+                           "parallelism": f"frame-parallel x{world}"},
+                "stream": leg}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if args.mode == "bands":
+        init_dist()
+        return bands_mode(args, world, rank, dev)
+
+    default_run = (args.workload == "1080p" and not args.iters and not args.batch and
+                   args.window == 5 and args.alpha == 1.0 and not args.levels)
+    if args.kb:
+        hsflow.set_iters_per_launch(args.kb)
+    prim = resident_leg(args.workload, args, dev, world, rank, init_dist)
+    sec = None
+    if default_run and not args.no_secondary:
+        sec = resident_leg("4k", args, dev, world, rank)
+    e2e = None
+    if not args.no_e2e and args.workload != "8k" and rank == 0:
+        e2e = e2e_leg(args.workload, args, dev)
+    strm = None
+    if not args.no_stream and args.workload == "1080p":
+        strm = stream_leg("1080p", args, world, rank, dev)
+
+    cpu = cpu_all = None
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(prim["rows"], prim["cols"], args.window, args.alpha,
+                           args.cpu_iters)
+        # SURVEY §8(d) second CPU line: all cores of the box's CPU share
+        # (16 per GPU on the MI355X pool; os.cpu_count() shows the machine)
+        n_thr = min(16, os.cpu_count() or 1)
+        cpu_all = cpu_baseline(prim["rows"], prim["cols"], args.window, args.alpha,
+                               args.cpu_iters, n_thr)
+
+    status = 0
+    if rank == 0:
+        line = {
+            "metric": "Mpix*iter/s (Horn-Schunck Jacobi) + frame-pairs/s",
+            "value": prim["value"],
+            "unit": "Mpix*iter/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": prim["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic {prim['input_dtype']} frame pairs (hash texture, shift "
+                    "(-0.75,+1.5) px)",
+            "config": {k: prim[k] for k in ("workload", "rows", "cols", "iters", "window",
+                                            "levels", "input_dtype", "alpha",
+                                            "pairs_per_gpu_per_step", "step")},
+            "pairs_per_s_resident": prim["pairs_per_s_resident"],
+            "parity": prim["parity"],
+            "roofline": prim["roofline"],
+            "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
+        }
+        line["config"]["parallelism"] = f"frame-parallel x{world}"
+        line["config"]["iters_per_launch"] = prim["roofline"]["iters_per_launch"]
+        if e2e is not None:
+            line.update(e2e)
+        if sec is not None:
+            line["secondary"] = {k: sec[k] for k in ("workload", "value", "ms_per_step",
+                                                     "pairs_per_s_resident", "roofline",
+                                                     "parity")}
+            line["secondary"]["unit"] = "Mpix*iter/s"
+        if strm is not None:
+            line["stream"] = strm
+        print(json.dumps(line), flush=True)
+        for leg in (prim, sec):
+            if leg is not None and leg["parity"] is not None and leg["parity"]["ok"] is False:
+                print(f"bench: PARITY FAILURE on {leg['workload']}: {leg['parity']}",
+                      file=sys.stderr)
+                status = 3
     if world > 1:
         dist.destroy_process_group()
+    if status:
+        sys.exit(status)
 
 
 def bands_mode(args, world, rank, dev):
@@ -390,29 +623,19 @@ def bands_mode(args, world, rank, dev):
     p = rb.plan(rows, cols, levels, world, args.window, args.chunk)
     ops = [rb.DeviceOps(args.window, args.alpha, dev)]
     comm = rb.DistComm() if world > 1 else rb.LocalComm()
+    res = [None]
 
     def one():
         states = rb.solve([I0], [I1], p, iters, ops, comm, [rank])
-        return rb.gather_owned(states, p, comm)
+        res[0] = rb.gather_owned(states, p, comm)
 
-    for _ in range(args.warmup):
-        one()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        u, v = one()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_region(one, lambda: torch.cuda.synchronize(dev), args.steps, args.warmup,
+                           world, dev)
     px_all = sum(r * c for r, c in p.sizes)
     if rank == 0:
-        ok = bool(torch.isfinite(u).all().item()) and 0.05 < float(u.mean()) < 0.3
+        u, v = res[0]
+        golden = golden_entry(rows, cols, iters, args.window, levels, args.alpha)
+        parity = parity_check(u.cpu().numpy(), v.cpu().numpy(), golden)
         print(json.dumps({
             "metric": "Mpix*iter/s (config 5: one pair in row bands, halo exchange over RCCL)",
             "value": round(px_all * iters * args.steps / elapsed / 1e6, 1),
@@ -423,7 +646,7 @@ def bands_mode(args, world, rank, dev):
             "config": {"workload": f"{cols}x{rows}, {levels} levels, {iters} it/level",
                        "window": args.window, "chunk": args.chunk, "halo_rows": p.halo,
                        "parallelism": f"row bands x{world}"},
-            "sane": ok}), flush=True)
+            "parity": parity}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -44,15 +44,12 @@ namespace {
 
 thread_local std::string g_err;  // errors from calls without a context
 int g_kb_override = 0;
-// Jacobi pass kernel: 0 = automatic, 2 = K2 tiles, 3 = K3 streaming strips
-// (hsflow_set_jacobi_kernel; HSFLOW_JACOBI sets the process default)
+// Jacobi pass kernel: 0 = automatic, 2 = K2 tiles, one launch per pass
+// (hsflow_set_jacobi_kernel; probe build: HSFLOW_JACOBI sets the default)
 int g_kernel_override = -1;
 
 int jacobi_kernel_choice() {
-    if (g_kernel_override < 0) {
-        const char *e = getenv("HSFLOW_JACOBI");
-        g_kernel_override = e ? atoi(e) : 0;
-    }
+    if (g_kernel_override < 0) g_kernel_override = hsflow::probe_env("HSFLOW_JACOBI", 0);
     return g_kernel_override;
 }
 
@@ -157,6 +154,26 @@ int pick_kb(int window, bool need_f32) {
 // (scripts/streams_ab.sh).  Fork and join are event based (capturable into a
 // hipGraph).  Never destroyed: they live until the process exits (no
 // static-destruction-order hazards).
+// The *_device entry points run on the device their stream belongs to
+// (the current device for the null stream), whatever device the calling
+// thread has current: side streams, the CU count and the launches all follow
+// the caller's stream.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(hipStream_t s) {
+        int cur = 0;
+        hipDevice_t d = 0;
+        if (!s || hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(s, &d) != hipSuccess)
+            return;
+        if (d != cur && hipSetDevice(d) == hipSuccess) prev = cur;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 struct SidePool {
     int device = -1;
     std::vector<hipStream_t> streams;
@@ -166,9 +183,8 @@ struct SidePool {
 int g_split_override = 0;
 
 int max_split() {
-    static const int n = [] {
-        const char *e = getenv("HSFLOW_STREAMS");
-        int k = e ? atoi(e) : 2;
+    static const int n = [] {  // probe build: HSFLOW_STREAMS
+        int k = hsflow::probe_env("HSFLOW_STREAMS", 2);
         return k < 1 ? 1 : (k > 16 ? 16 : k);
     }();
     return g_split_override > 0 ? g_split_override : n;
@@ -265,11 +281,8 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
     a.gy = w.gy;
     a.gt = w.gt;
     a.flags = w.flags;
-    static const int ablate = [] {
-        const char *e = getenv("HSFLOW_ABLATE");
-        return e ? atoi(e) : 0;
-    }();
-    a.ablate = ablate;
+    static const int ablate = hsflow::probe_env("HSFLOW_ABLATE", 0);
+    a.ablate = ablate;  // the product kernels ignore it (compiled out)
     // pass p writes the caller's buffers iff (passes-1-p) is even, so the
     // last pass always lands in (u, v)
     auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };
@@ -292,12 +305,7 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         a.v_in = src_v;
         a.u_out = dst_is_user(pass) ? u : w.u2;
         a.v_out = dst_is_user(pass) ? v : w.v2;
-        // K3 and K2 give identical bits, so passes may mix (K3 runs full
-        // passes of even-width images only)
-        const int kc = jacobi_kernel_choice();
-        const bool k3 = kc == 3 && a.iters == kb && hsflow::k3_supported(window, kb, cols);
-        hipError_t e = k3 ? hsflow::launch_jacobi_stream(a, window, kb, s)
-                          : hsflow::launch_jacobi(a, window, kb, s);
+        hipError_t e = hsflow::launch_jacobi(a, window, kb, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "jacobi launch");
         src_u = a.u_out;
         src_v = a.v_out;
@@ -483,15 +491,17 @@ int download_planes(hsflow_ctx *ctx, const float *const *src, void *const *dst, 
 }
 
 int check_host_args(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
-                    int rows, int cols, size_t in_step, int dtype_out, size_t out_step) {
+                    int rows, int cols, size_t step0, size_t step1, int dtype_out,
+                    size_t out_step) {
     if (!ctx) return HSFLOW_ERR_ARG;
     if (!I0 || !I1) return fail(ctx, HSFLOW_ERR_ARG, "null image");
     if (!sizes_ok(rows, cols, 1))
         return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d", rows, cols);
     const int es = elem_size(dtype_in);
     if (!es) return fail(ctx, HSFLOW_ERR_ARG, "unsupported input dtype %d", dtype_in);
-    if (in_step < (size_t)cols * es)
-        return fail(ctx, HSFLOW_ERR_ARG, "input step %zu < row bytes", in_step);
+    if (step0 < (size_t)cols * es || step1 < (size_t)cols * es)
+        return fail(ctx, HSFLOW_ERR_ARG, "input steps %zu, %zu < row bytes %zu", step0, step1,
+                    (size_t)cols * es);
     if (dtype_out != HSFLOW_F32 && dtype_out != HSFLOW_F64)
         return fail(ctx, HSFLOW_ERR_ARG, "output dtype must be F32 or F64");
     if (out_step < (size_t)cols * elem_size(dtype_out))
@@ -598,6 +608,8 @@ extern "C" {
 
 int hsflow_version(void) { return HSFLOW_VERSION; }
 
+int hsflow_build_flags(void) { return hsflow::kProbeBuild ? HSFLOW_BUILD_PROBE : 0; }
+
 const char *hsflow_status_string(int status) {
     switch (status) {
     case HSFLOW_OK: return "ok";
@@ -667,7 +679,7 @@ int hsflow_set_iters_per_launch(int k) {
 }
 
 int hsflow_set_jacobi_kernel(int k) {
-    if (k != 0 && k != 2 && k != 3) return HSFLOW_ERR_ARG;
+    if (k != 0 && k != 2) return HSFLOW_ERR_ARG;
     g_kernel_override = k;
     return HSFLOW_OK;
 }
@@ -689,6 +701,7 @@ int hsflow_iters_per_launch(int rows, int cols, int batch, int window) {
 int hsflow_gradients_device(const void *I0, const void *I1, int dtype_in, int rows,
                             int cols, int batch, float *gx, float *gy, float *gt,
                             void *workspace, size_t workspace_bytes, void *stream) {
+    DeviceGuard g((hipStream_t)stream);
     return gradients_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, gx, gy, gt,
                           workspace, workspace_bytes, (hipStream_t)stream);
 }
@@ -696,6 +709,7 @@ int hsflow_gradients_device(const void *I0, const void *I1, int dtype_in, int ro
 int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
                          float alpha, int warm_start, float *u, float *v, void *workspace,
                          size_t workspace_bytes, void *stream) {
+    DeviceGuard g((hipStream_t)stream);
     // the workspace flags say per pair which gradient format is valid; the
     // f32 variant is launched too unless we know every pair is packed
     return jacobi_impl(nullptr, rows, cols, batch, window, iters, alpha, warm_start != 0,
@@ -705,6 +719,7 @@ int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
 int hsflow_flow_device(const void *I0, const void *I1, int dtype_in, int rows, int cols,
                        int batch, int window, int iters, float alpha, float *u, float *v,
                        void *workspace, size_t workspace_bytes, void *stream) {
+    DeviceGuard g((hipStream_t)stream);
     int rc = gradients_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, nullptr,
                             nullptr, nullptr, workspace, workspace_bytes,
                             (hipStream_t)stream);
@@ -716,10 +731,10 @@ int hsflow_flow_device(const void *I0, const void *I1, int dtype_in, int rows, i
 }
 
 int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, int rows,
-                int cols, size_t in_step, int window, int iters, double alpha, void *u,
-                void *v, int dtype_out, size_t out_step) {
-    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step, dtype_out,
-                             out_step);
+                int cols, size_t in_step0, size_t in_step1, int window, int iters,
+                double alpha, void *u, void *v, int dtype_out, size_t out_step) {
+    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step0, in_step1,
+                             dtype_out, out_step);
     if (rc) return rc;
     if (!u || !v) return fail(ctx, HSFLOW_ERR_ARG, "null output");
     if (window < 1 || window > HSFLOW_MAX_WINDOW)
@@ -736,8 +751,8 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
     float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
     int dt0 = 0, dt1 = 0;
-    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step, in0, &dt0))) return rc;
-    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step, in1, &dt1))) return rc;
+    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step0, in0, &dt0))) return rc;
+    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step1, in1, &dt1))) return rc;
     rc = gradients_impl(ctx, in0, in1, dt0, rows, cols, 1, nullptr, nullptr, nullptr,
                         ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
@@ -783,6 +798,7 @@ int hsflow_pyramid_build_device(const void *I0, const void *I1, int dtype_in, in
         if (!I0_levels[l - 1] || !I1_levels[l - 1])
             return fail(nullptr, HSFLOW_ERR_ARG, "null level plane %d", l);
     hipStream_t s = (hipStream_t)stream;
+    DeviceGuard g(s);
     // K1 at level 0 decides each pair's rounding (flags in the workspace)
     int rc = gradients_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, nullptr, nullptr,
                             nullptr, workspace, workspace_bytes, s);
@@ -806,6 +822,7 @@ int hsflow_pyramid_build_device(const void *I0, const void *I1, int dtype_in, in
 
 int hsflow_upflow_device(const float *uc, const float *vc, int rc, int cc, float *u,
                          float *v, int rows, int cols, int batch, void *stream) {
+    DeviceGuard g((hipStream_t)stream);
     if (!uc || !vc || !u || !v) return fail(nullptr, HSFLOW_ERR_ARG, "null device pointer");
     if (!sizes_ok(rows, cols, batch) || rc < (rows + 1) / 2 || cc < (cols + 1) / 2)
         return fail(nullptr, HSFLOW_ERR_ARG, "bad sizes %dx%d from %dx%d", rows, cols, rc, cc);
@@ -819,16 +836,17 @@ int hsflow_flow_pyramid_device(const void *I0, const void *I1, int dtype_in, int
                                int cols, int batch, int levels, int window, int iters,
                                float alpha, float *u, float *v, void *workspace,
                                size_t workspace_bytes, void *stream) {
+    DeviceGuard g((hipStream_t)stream);
     return pyramid_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, levels, window, iters,
                         alpha, u, v, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
-                        int rows, int cols, size_t in_step, int levels, int window,
-                        int iters, double alpha, void *u, void *v, int dtype_out,
-                        size_t out_step) {
-    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step, dtype_out,
-                             out_step);
+                        int rows, int cols, size_t in_step0, size_t in_step1, int levels,
+                        int window, int iters, double alpha, void *u, void *v,
+                        int dtype_out, size_t out_step) {
+    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step0, in_step1,
+                             dtype_out, out_step);
     if (rc) return rc;
     if (!u || !v) return fail(ctx, HSFLOW_ERR_ARG, "null output");
     if (levels < 1 || levels > HSFLOW_MAX_LEVELS)
@@ -844,8 +862,8 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
     char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
     float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
     int dt0 = 0, dt1 = 0;
-    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step, in0, &dt0))) return rc;
-    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step, in1, &dt1))) return rc;
+    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step0, in0, &dt0))) return rc;
+    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step1, in1, &dt1))) return rc;
     rc = pyramid_impl(ctx, in0, in1, dt0, rows, cols, 1, levels, window, iters,
                       (float)alpha, du, dv, ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
@@ -860,6 +878,7 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
 
 int hsflow_bgr_to_gray_device(const uint8_t *bgr, int rows, int cols, int batch,
                               uint8_t *gray, void *stream) {
+    DeviceGuard g((hipStream_t)stream);
     if (!bgr || !gray) return fail(nullptr, HSFLOW_ERR_ARG, "null device pointer");
     if (!sizes_ok(rows, cols, batch))
         return fail(nullptr, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
@@ -869,13 +888,14 @@ int hsflow_bgr_to_gray_device(const uint8_t *bgr, int rows, int cols, int batch,
 }
 
 int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, int rows,
-                    int cols, size_t bgr_step, int window, int iters, double alpha,
-                    void *u, void *v, int dtype_out, size_t out_step) {
+                    int cols, size_t bgr_step0, size_t bgr_step1, int window, int iters,
+                    double alpha, void *u, void *v, int dtype_out, size_t out_step) {
     if (!ctx) return HSFLOW_ERR_ARG;
     if (!bgr0 || !bgr1 || !u || !v) return fail(ctx, HSFLOW_ERR_ARG, "null pointer");
     if (!sizes_ok(rows, cols, 1)) return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d", rows, cols);
-    if (bgr_step < (size_t)cols * 3)
-        return fail(ctx, HSFLOW_ERR_ARG, "BGR step %zu < row bytes", bgr_step);
+    if (bgr_step0 < (size_t)cols * 3 || bgr_step1 < (size_t)cols * 3)
+        return fail(ctx, HSFLOW_ERR_ARG, "BGR steps %zu, %zu < row bytes", bgr_step0,
+                    bgr_step1);
     if (dtype_out != HSFLOW_F32 && dtype_out != HSFLOW_F64)
         return fail(ctx, HSFLOW_ERR_ARG, "output dtype must be F32 or F64");
     if (out_step < (size_t)cols * elem_size(dtype_out))
@@ -894,9 +914,9 @@ int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, i
     if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, hsflow_workspace_bytes(rows, cols, 1))))
         return rc;
     uint8_t *db = (uint8_t *)ctx->d_in, *dg = db + gray_off;
-    HIP_TRY(ctx, hipMemcpy2DAsync(db, (size_t)cols * 3, bgr0, bgr_step, (size_t)cols * 3, rows,
-                                  hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpy2DAsync(db + 3 * n, (size_t)cols * 3, bgr1, bgr_step,
+    HIP_TRY(ctx, hipMemcpy2DAsync(db, (size_t)cols * 3, bgr0, bgr_step0, (size_t)cols * 3,
+                                  rows, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(db + 3 * n, (size_t)cols * 3, bgr1, bgr_step1,
                                   (size_t)cols * 3, rows, hipMemcpyHostToDevice, ctx->stream));
     hipError_t e = hsflow::launch_bgr2gray(db, rows, cols, 2, dg, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "bgr2gray launch");
@@ -917,10 +937,10 @@ int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, i
 }
 
 int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
-                     int rows, int cols, size_t in_step, void *gx, void *gy, void *gt,
-                     int dtype_out, size_t out_step) {
-    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step, dtype_out,
-                             out_step);
+                     int rows, int cols, size_t in_step0, size_t in_step1, void *gx,
+                     void *gy, void *gt, int dtype_out, size_t out_step) {
+    int rc = check_host_args(ctx, I0, I1, dtype_in, rows, cols, in_step0, in_step1,
+                             dtype_out, out_step);
     if (rc) return rc;
     if (!gx || !gy || !gt) return fail(ctx, HSFLOW_ERR_ARG, "null output");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -935,8 +955,8 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
     float *dy = (float *)((char *)dx + align_up(n * 4));
     float *dt = (float *)((char *)dy + align_up(n * 4));
     int dt0 = 0, dt1 = 0;
-    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step, in0, &dt0))) return rc;
-    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step, in1, &dt1))) return rc;
+    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step0, in0, &dt0))) return rc;
+    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step1, in1, &dt1))) return rc;
     rc = gradients_impl(ctx, in0, in1, dt0, rows, cols, 1, dx, dy, dt, ctx->d_ws,
                         ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;

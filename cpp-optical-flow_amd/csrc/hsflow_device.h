@@ -1,7 +1,7 @@
-// hsflow_device.h -- device helpers shared by the Jacobi kernels (K2 tiles in
-// hsflow_kernels.hip, K3 streaming strips in hsflow_stream.hip).  Both build
+// hsflow_device.h -- device helpers shared by the Jacobi kernels (K2 tiles and
+// their persistent dataflow form in hsflow_kernels.hip).  Every variant builds
 // the per-pixel operation sequence of hornSchunck.cpp:56-74 from these same
-// functions, so the two kernels give bit-identical (u, v).
+// functions, so they all give bit-identical (u, v).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -2,8 +2,28 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace hsflow {
+
+// Diagnostic environment switches (HSFLOW_K2_TL, HSFLOW_ABLATE, ...) exist
+// only in the probe build (`make probe` -> libhsflow_probe.so, compiled with
+// -DHSFLOW_PROBE).  The product library never reads the environment, so no
+// variable can change the work a caller (or bench.py) times.
+#ifdef HSFLOW_PROBE
+constexpr bool kProbeBuild = true;
+#else
+constexpr bool kProbeBuild = false;
+#endif
+inline int probe_env(const char *name, int dflt) {
+#ifdef HSFLOW_PROBE
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
+}
 
 // Arguments of one Jacobi launch (hornSchunck.cpp:56-74 x `iters`).
 struct JacobiArgs {
@@ -17,10 +37,10 @@ struct JacobiArgs {
     const uint32_t *gpack;     // packed exact integer gradients
     const float *gx, *gy, *gt; // f32 gradients (non-integral inputs)
     const uint32_t *flags;     // per pair: 0 -> gpack valid, else f32 planes
-    int ablate;                // diagnostics only (HSFLOW_ABLATE): 1 = no
+    int ablate;                // probe build only (HSFLOW_ABLATE): 1 = no
                                // iterations (memory only), 2 = no memory
-                               // traffic (descriptors of size 0)
-    int seg_rows;              // K3: output rows per segment (launcher)
+                               // traffic (descriptors of size 0); always 0
+                               // in the product library
     int band_w;                // K2 workgroup kernel: tile-column band width
                                // of the tile order (0 = row-major; launcher)
 };
@@ -29,9 +49,6 @@ hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int ro
                             int cols, int batch, uint32_t *gpack, float *gx, float *gy,
                             float *gt, uint32_t *flags, hipStream_t s);
 hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s);
-// K3 streaming pass (hsflow_stream.hip): exactly KB iterations, even widths
-hipError_t launch_jacobi_stream(JacobiArgs a, int W, int KB, hipStream_t s);
-bool k3_supported(int W, int KB, int cols);
 // config 5 pyramid (hsflow_pyramid.hip); dtype as HSFLOW_U8/F32/F16
 hipError_t launch_pyrdown(const void *src, int dtype, int rows, int cols, int batch,
                           float *dst, const uint32_t *flags, hipStream_t s);

@@ -511,7 +511,8 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         rowmask |= (uint64_t)((unsigned)(r0 + r) < (unsigned)p.rows) << r;
 
     constexpr int kOOB = 0x7FFFFFF0;
-    const int nbytes = p.ablate == 2 ? 0 : plane_bytes;
+    const int ablate = kProbeBuild ? p.ablate : 0;  // compiled out of the product
+    const int nbytes = ablate == 2 ? 0 : plane_bytes;
     const auto u_rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase), 0, p.u_in ? nbytes : 0,
         0x00020000);
@@ -615,7 +616,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         hv = f2v{c, d};
     };
 
-    const int n_it = p.ablate == 1 ? 0 : p.iters;
+    const int n_it = ablate == 1 ? 0 : p.iters;
     // The vertical sums follow the parity of the image row (PAR = parity
     // of slab row 0), so every slab height, blocking depth and kernel
     // adds in the same order.  w = 5: pair sums Q(t) = h(t) + h(t+1) at
@@ -871,13 +872,10 @@ static hipError_t launch_jacobi_t(JacobiArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// K2 variant (HSFLOW_K2 env, diagnostics): 0 = per-wave regions
+// K2 variant (HSFLOW_K2, probe build only): 0 = per-wave regions
 // (hs_jacobi_kernel) for every window; otherwise the workgroup kernel.
 static int k2_variant() {
-    static int v = [] {
-        const char *e = getenv("HSFLOW_K2");
-        return e ? atoi(e) : 88;
-    }();
+    static const int v = probe_env("HSFLOW_K2", 88);
     return v;
 }
 
@@ -951,18 +949,12 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     a.tiles_y = (a.rows + OY - 1) / OY;
     const long ntiles = (long)a.tiles_x * a.tiles_y;
     dim3 grd((unsigned)ntiles, (unsigned)a.batch, 1);
-    // tile order: HSFLOW_K2_BAND = band width in tiles (0: row-major)
-    static const int band_env = [] {
-        const char *e = getenv("HSFLOW_K2_BAND");
-        return e ? atoi(e) : 0;
-    }();
+    // probe build only: HSFLOW_K2_BAND = tile order in bands of that many
+    // tile columns (0: row-major); HSFLOW_EXTRA_LDS = bytes of unused dynamic
+    // LDS per workgroup (lowers the workgroups per CU, occupancy probes)
+    static const int band_env = probe_env("HSFLOW_K2_BAND", 0);
     a.band_w = band_env;
-    // diagnostics: HSFLOW_EXTRA_LDS bytes of unused dynamic LDS per workgroup
-    // (lowers the workgroups per CU; used to measure occupancy sensitivity)
-    static const unsigned extra_lds = [] {
-        const char *e = getenv("HSFLOW_EXTRA_LDS");
-        return e ? (unsigned)atoi(e) : 0u;
-    }();
+    static const unsigned extra_lds = (unsigned)probe_env("HSFLOW_EXTRA_LDS", 0);
     hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW, SB>), grd, dim3(NW * 64),
                        extra_lds, s, a);
     return hipGetLastError();
@@ -987,14 +979,11 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     // Taller slabs with the T plane in LDS (wg_rows_tl): w = 5, 11 rows
     // (88 x 128 region), single-buffered exchange: same box, 1080p x 8 /
     // 4K x 2, 1.011 M / 1.072 M -> 1.032 M / 1.089 M Mpix*iter/s (12 rows
-    // spill).  HSFLOW_K2_TL=0 keeps the all-register slabs everywhere,
+    // spill).  Probe build: HSFLOW_K2_TL=0 keeps the all-register slabs everywhere,
     // =1 uses the taller ones for every window that has them; default w = 5
     // and w = 6 (8 -> 10 rows: 1080p 782 k -> 859 k, 4K 793 k -> 891 k);
     // at w = 3 and w = 4 they measure equal to the all-register slabs.
-    static const int tl_env = [] {
-        const char *e = getenv("HSFLOW_K2_TL");
-        return e ? atoi(e) : -1;
-    }();
+    static const int tl_env = probe_env("HSFLOW_K2_TL", -1);
     constexpr int RT = wg_rows_tl(W);
     if constexpr (RT > 0 && KB * (W - 1) < 8 * RT / 2) {
         bool on = tl_env < 0 ? (W == 5 || W == 6) : tl_env != 0;

@@ -118,6 +118,7 @@ class RawVideo:
 
 class Y4MVideo:
     _CHROMA = {"444": (1, 1), "422": (2, 1), "420": (2, 2), "411": (4, 1), "mono": None}
+    _SUFFIX_420 = ("", "jpeg", "paldv", "mpeg2")
 
     def __init__(self, path: str):
         self.path = path
@@ -130,8 +131,15 @@ class Y4MVideo:
             self.cols, self.rows = int(d["W"]), int(d["H"])
             cs = d.get("C", "420jpeg")
             key = "mono" if cs.startswith("mono") else cs[:3]
+            suffix = cs[len(key):]
             if key not in self._CHROMA:
                 raise FrameError(f"{path}: chroma {cs} unsupported")
+            # 8-bit sample layouts only: 420jpeg/paldv/mpeg2 differ in chroma
+            # siting, not size; C420p10, C444p12, Cmono16 ... hold 16-bit
+            # samples and 444alpha a fourth plane
+            if suffix not in (self._SUFFIX_420 if key == "420" else ("",)):
+                raise FrameError(f"{path}: chroma {cs} unsupported (8-bit "
+                                 f"{'/'.join(sorted(self._CHROMA))} only)")
             sub = self._CHROMA[key]
             self.full_range = "XCOLORRANGE=FULL" in params
             luma = self.rows * self.cols

@@ -50,8 +50,9 @@ EXPORTS = (
     "hsflow_pyramid_level_size", "hsflow_pyramid_workspace_bytes",
     "hsflow_flow_pyramid_device", "hsflow_flow_pyramid", "hsflow_bgr_to_gray_device",
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
-    "hsflow_set_jacobi_kernel",
+    "hsflow_set_jacobi_kernel", "hsflow_build_flags",
 )
+BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
 
 
 class HsflowError(RuntimeError):
@@ -93,9 +94,11 @@ def lib():
     L.hsflow_last_error.restype = ctypes.c_char_p
     L.hsflow_stream.argtypes = [_vp]
     L.hsflow_stream.restype = _vp
-    L.hsflow_flow.argtypes = [_vp, _vp, _vp, i, i, i, _sz, i, i, ctypes.c_double,
+    L.hsflow_build_flags.restype = i
+    L.hsflow_flow.argtypes = [_vp, _vp, _vp, i, i, i, _sz, _sz, i, i, ctypes.c_double,
                               _vp, _vp, i, _sz]
-    L.hsflow_gradients.argtypes = [_vp, _vp, _vp, i, i, i, _sz, _vp, _vp, _vp, i, _sz]
+    L.hsflow_gradients.argtypes = [_vp, _vp, _vp, i, i, i, _sz, _sz, _vp, _vp, _vp, i,
+                                   _sz]
     L.hsflow_workspace_bytes.argtypes = [i, i, i]
     L.hsflow_workspace_bytes.restype = _sz
     L.hsflow_flow_device.argtypes = [_vp, _vp, i, i, i, i, i, i, ctypes.c_float,
@@ -113,15 +116,15 @@ def lib():
     L.hsflow_pyramid_workspace_bytes.restype = _sz
     L.hsflow_flow_pyramid_device.argtypes = [_vp, _vp, i, i, i, i, i, i, i,
                                              ctypes.c_float, _vp, _vp, _vp, _sz, _vp]
-    L.hsflow_flow_pyramid.argtypes = [_vp, _vp, _vp, i, i, i, _sz, i, i, i,
+    L.hsflow_flow_pyramid.argtypes = [_vp, _vp, _vp, i, i, i, _sz, _sz, i, i, i,
                                       ctypes.c_double, _vp, _vp, i, _sz]
     L.hsflow_pyramid_build_device.argtypes = [_vp, _vp, i, i, i, i, i,
                                               ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                               _vp, _sz, _vp]
     L.hsflow_upflow_device.argtypes = [_vp, _vp, i, i, _vp, _vp, i, i, i, _vp]
     L.hsflow_bgr_to_gray_device.argtypes = [_vp, i, i, i, _vp, _vp]
-    L.hsflow_flow_bgr.argtypes = [_vp, _vp, _vp, i, i, _sz, i, i, ctypes.c_double, _vp,
-                                  _vp, i, _sz]
+    L.hsflow_flow_bgr.argtypes = [_vp, _vp, _vp, i, i, _sz, _sz, i, i, ctypes.c_double,
+                                  _vp, _vp, i, _sz]
     L.hsflow_bgr_to_gray.argtypes = [_vp, i, i, _sz, _vp, _sz]
     L.hsflow_synth_pair.argtypes = [ctypes.c_uint64, i, i, i, i, _vp, _vp, _vp, _vp]
     _lib = L
@@ -145,6 +148,15 @@ def _dtype_code(a: np.ndarray) -> int:
     if a.dtype == np.float16:
         return F16
     raise HsflowError(HSFLOW_ERR_ARG, f"unsupported image dtype {a.dtype}")
+
+
+def _common_dtype(a, b):
+    """Frames of different element types are both widened to float64, as
+    hornSchunck.cpp:23-24 converts each with convertTo(CV_64FC1); each frame
+    keeps its own row step."""
+    if a.dtype != b.dtype:
+        return a.astype(np.float64), b.astype(np.float64)
+    return a, b
 
 
 def _as_image(a) -> np.ndarray:
@@ -188,14 +200,14 @@ class Context:
         a, b = _as_image(I0), _as_image(I1)
         if a.shape != b.shape:
             raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
-        if a.dtype != b.dtype:
-            b = b.astype(a.dtype)
+        a, b = _common_dtype(a, b)
         rows, cols = a.shape
         u = np.empty((rows, cols), out_dtype)
         v = np.empty((rows, cols), out_dtype)
         code = F64 if u.dtype == np.float64 else F32
         rc = lib().hsflow_flow(self._p, a.ctypes.data, b.ctypes.data, _dtype_code(a),
-                               rows, cols, a.strides[0], int(window), int(iters),
+                               rows, cols, a.strides[0], b.strides[0], int(window),
+                               int(iters),
                                float(alpha), u.ctypes.data, v.ctypes.data, code,
                                u.strides[0])
         _check(rc, self._p)
@@ -208,15 +220,14 @@ class Context:
         a, b = _as_image(I0), _as_image(I1)
         if a.shape != b.shape:
             raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
-        if a.dtype != b.dtype:
-            b = b.astype(a.dtype)
+        a, b = _common_dtype(a, b)
         rows, cols = a.shape
         u = np.empty((rows, cols), out_dtype)
         v = np.empty((rows, cols), out_dtype)
         code = F64 if u.dtype == np.float64 else F32
         rc = lib().hsflow_flow_pyramid(self._p, a.ctypes.data, b.ctypes.data,
                                        _dtype_code(a), rows, cols, a.strides[0],
-                                       int(levels), int(window), int(iters), float(alpha),
+                                       b.strides[0], int(levels), int(window), int(iters), float(alpha),
                                        u.ctypes.data, v.ctypes.data, code, u.strides[0])
         _check(rc, self._p)
         return u, v
@@ -232,14 +243,16 @@ class Context:
                 raise HsflowError(HSFLOW_ERR_ARG, "need H x W x 3 BGR uint8")
         if a.shape != b.shape:
             raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
-        if a.strides[1:] != (3, 1) or b.strides[0] != a.strides[0]:
-            a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+        if a.strides[1:] != (3, 1) or a.strides[0] < 3 * a.shape[1]:
+            a = np.ascontiguousarray(a)
+        if b.strides[1:] != (3, 1) or b.strides[0] < 3 * b.shape[1]:
+            b = np.ascontiguousarray(b)
         rows, cols = a.shape[:2]
         u = np.empty((rows, cols), out_dtype)
         v = np.empty((rows, cols), out_dtype)
         code = F64 if u.dtype == np.float64 else F32
         rc = lib().hsflow_flow_bgr(self._p, a.ctypes.data, b.ctypes.data, rows, cols,
-                                   a.strides[0], int(window), int(iters), float(alpha),
+                                   a.strides[0], b.strides[0], int(window), int(iters), float(alpha),
                                    u.ctypes.data, v.ctypes.data, code, u.strides[0])
         _check(rc, self._p)
         return u, v
@@ -248,13 +261,12 @@ class Context:
         a, b = _as_image(I0), _as_image(I1)
         if a.shape != b.shape:
             raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
-        if a.dtype != b.dtype:
-            b = b.astype(a.dtype)
+        a, b = _common_dtype(a, b)
         rows, cols = a.shape
         gx, gy, gt = (np.empty((rows, cols), out_dtype) for _ in range(3))
         code = F64 if gx.dtype == np.float64 else F32
         rc = lib().hsflow_gradients(self._p, a.ctypes.data, b.ctypes.data, _dtype_code(a),
-                                    rows, cols, a.strides[0], gx.ctypes.data,
+                                    rows, cols, a.strides[0], b.strides[0], gx.ctypes.data,
                                     gy.ctypes.data, gt.ctypes.data, code, gx.strides[0])
         _check(rc, self._p)
         return gx, gy, gt
@@ -313,10 +325,21 @@ def compute(I0, I1, alpha: float, nIter: int, windowSize: int = 5, levels: int =
 
 
 # ------------------------------------------------------------ device (torch)
-def _stream_ptr(stream):
+def _stream_ptr(stream, device=None):
+    """hipStream_t of `stream`, or of the current stream of `device` (the
+    tensors' device) when stream is None; the library runs each call on the
+    device its stream belongs to."""
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream if torch is not None else None
+        return torch.cuda.current_stream(device).cuda_stream if torch is not None else None
     return getattr(stream, "cuda_stream", stream)
+
+
+def build_flags() -> int:
+    return int(lib().hsflow_build_flags())
+
+
+def is_probe_build() -> bool:
+    return bool(build_flags() & BUILD_PROBE)
 
 
 def workspace_bytes(rows: int, cols: int, batch: int = 1) -> int:
@@ -345,6 +368,16 @@ def _check_dense(t, shape, name):
                           f"[..., {shape[0]}, {shape[1]}]")
 
 
+def _check_plane(t, shape, batch, name):
+    """u, v (and the warm-start planes) are written by the kernels through
+    raw pointers: a float32, contiguous CUDA tensor holding at least
+    batch x rows x cols elements, or HsflowError (not a GPU fault)."""
+    if t is None or not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous() or \
+            tuple(t.shape[-2:]) != tuple(shape) or t.numel() < batch * shape[0] * shape[1]:
+        raise HsflowError(HSFLOW_ERR_ARG, f"{name}: need a contiguous float32 CUDA tensor of "
+                          f"{batch} x {shape[0]} x {shape[1]}")
+
+
 def flow_device(I0, I1, window: int, iters: int, alpha: float, u=None, v=None,
                 workspace=None, stream=None):
     """Stream-ordered solve on torch CUDA tensors [B, H, W] (or [H, W]).
@@ -359,12 +392,14 @@ def flow_device(I0, I1, window: int, iters: int, alpha: float, u=None, v=None,
         u = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
     if v is None:
         v = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
+    _check_plane(u, (rows, cols), batch, "u")
+    _check_plane(v, (rows, cols), batch, "v")
     if workspace is None:
         workspace = alloc_workspace(rows, cols, batch, I0.device)
     rc = lib().hsflow_flow_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0), rows,
                                   cols, batch, int(window), int(iters), float(alpha),
                                   u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
-                                  workspace.numel(), _stream_ptr(stream))
+                                  workspace.numel(), _stream_ptr(stream, I0.device))
     _check(rc)
     return u, v
 
@@ -394,6 +429,8 @@ def flow_pyramid_device(I0, I1, levels: int, window: int, iters: int, alpha: flo
         u = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
     if v is None:
         v = torch.empty(I0.shape, dtype=torch.float32, device=I0.device)
+    _check_plane(u, (rows, cols), batch, "u")
+    _check_plane(v, (rows, cols), batch, "v")
     if workspace is None:
         n = pyramid_workspace_bytes(rows, cols, batch, levels)
         workspace = torch.empty(n, dtype=torch.uint8, device=I0.device)
@@ -401,7 +438,7 @@ def flow_pyramid_device(I0, I1, levels: int, window: int, iters: int, alpha: flo
                                           rows, cols, batch, int(levels), int(window),
                                           int(iters), float(alpha), u.data_ptr(),
                                           v.data_ptr(), workspace.data_ptr(),
-                                          workspace.numel(), _stream_ptr(stream))
+                                          workspace.numel(), _stream_ptr(stream, I0.device))
     _check(rc)
     return u, v
 
@@ -427,7 +464,7 @@ def pyramid_build_device(I0, I1, levels: int, workspace=None, stream=None):
     _check(lib().hsflow_pyramid_build_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
                                              rows, cols, batch, int(levels), a0, a1,
                                              workspace.data_ptr(), workspace.numel(),
-                                             _stream_ptr(stream)))
+                                             _stream_ptr(stream, I0.device)))
     return P0, P1
 
 
@@ -436,8 +473,12 @@ def upflow_device(uc, vc, u, v, stream=None):
     uc, vc are dense [rows, cols] / [rc, cc] views (row slices allowed)."""
     rc, cc = uc.shape[-2:]
     rows, cols = u.shape[-2:]
+    for t, name, shape in ((uc, "uc", (rc, cc)), (vc, "vc", (rc, cc)), (u, "u", (rows, cols)),
+                           (v, "v", (rows, cols))):
+        _check_plane(t, shape, 1, name)
     _check(lib().hsflow_upflow_device(uc.data_ptr(), vc.data_ptr(), rc, cc, u.data_ptr(),
-                                      v.data_ptr(), rows, cols, 1, _stream_ptr(stream)))
+                                      v.data_ptr(), rows, cols, 1,
+                                      _stream_ptr(stream, u.device)))
 
 
 def gradients_device(I0, I1, workspace, gx=None, gy=None, gt=None, stream=None):
@@ -449,16 +490,18 @@ def gradients_device(I0, I1, workspace, gx=None, gy=None, gt=None, stream=None):
     rc = lib().hsflow_gradients_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
                                        rows, cols, batch, ptr(gx), ptr(gy), ptr(gt),
                                        workspace.data_ptr(), workspace.numel(),
-                                       _stream_ptr(stream))
+                                       _stream_ptr(stream, I0.device))
     _check(rc)
 
 
 def jacobi_device(rows, cols, batch, window, iters, alpha, u, v, workspace,
                   warm_start=False, stream=None):
+    _check_plane(u, (rows, cols), batch, "u")
+    _check_plane(v, (rows, cols), batch, "v")
     rc = lib().hsflow_jacobi_device(int(rows), int(cols), int(batch), int(window),
                                     int(iters), float(alpha), int(bool(warm_start)),
                                     u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
-                                    workspace.numel(), _stream_ptr(stream))
+                                    workspace.numel(), _stream_ptr(stream, u.device))
     _check(rc)
 
 
@@ -503,8 +546,12 @@ def bgr_to_gray_device(bgr, gray=None, stream=None):
     batch = int(np.prod(bgr.shape[:-3])) if bgr.dim() > 3 else 1
     if gray is None:
         gray = torch.empty(bgr.shape[:-1], dtype=torch.uint8, device=bgr.device)
+    if gray.dtype != torch.uint8 or not gray.is_cuda or not gray.is_contiguous() or \
+            gray.numel() < batch * rows * cols or gray.device != bgr.device:
+        raise HsflowError(HSFLOW_ERR_ARG, "gray: need a contiguous uint8 CUDA tensor of "
+                          f"{batch} x {rows} x {cols} on {bgr.device}")
     _check(lib().hsflow_bgr_to_gray_device(bgr.data_ptr(), rows, cols, batch,
-                                           gray.data_ptr(), _stream_ptr(stream)))
+                                           gray.data_ptr(), _stream_ptr(stream, bgr.device)))
     return gray
 
 

@@ -51,7 +51,11 @@ class hornSchunck {
         sync_params();
         cv::Mat ha, hb;
         const hsflow::ImageView a = as_view(imagePrev, ha), b = as_view(imageNext, hb);
-        // hornSchunck.cpp:49-50: u, v are (re)allocated as CV_64FC1
+        // hornSchunck.cpp:49-50 and :72-73 assign MatExprs (Mat::zeros, then
+        // uAvg - uUpdateConst) to u, v; OpenCV evaluates a MatExpr into the
+        // destination through create(), so an existing CV_64FC1 buffer of the
+        // right size is written in place (headers sharing it see the result)
+        // and anything else is reallocated.  create() here does the same.
         u.create(imagePrev.rows, imagePrev.cols, CV_64FC1);
         v.create(imagePrev.rows, imagePrev.cols, CV_64FC1);
         if (u.step != v.step) CV_Error(cv::Error::StsInternal, "u/v steps differ");

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define HSFLOW_VERSION 10000 /* 1.0.0 */
+#define HSFLOW_VERSION 20000 /* 2.0.0: separate row steps for I0 and I1 */
 
 /* Status codes (0 ok, <0 error).  The reference has no codes: OpenCV throws
  * cv::Exception (e.g. size mismatch in multiply, hornSchunck.cpp:63-70);
@@ -66,6 +66,12 @@ typedef struct hsflow_ctx hsflow_ctx;
 int hsflow_version(void);
 const char *hsflow_status_string(int status);
 
+/* Build flags of the loaded library.  HSFLOW_BUILD_PROBE: the diagnostic
+ * build (`make probe`, libhsflow_probe.so) whose kernels honour HSFLOW_*
+ * environment switches; the product library ignores the environment. */
+#define HSFLOW_BUILD_PROBE 1
+int hsflow_build_flags(void);
+
 /* Context = device + stream + cached device buffers (grow-only). */
 int hsflow_create(hsflow_ctx **ctx, int device);
 void hsflow_destroy(hsflow_ctx *ctx);
@@ -76,23 +82,26 @@ void *hsflow_stream(hsflow_ctx *ctx);
 /* ---- host-buffer, blocking: the reference's two methods ---------------- */
 
 /* hornSchunck::getFlow (hornSchunck.cpp:43-75).  I0/I1: rows x cols, element
- * type dtype_in, row step in BYTES (cv::Mat::step; non-continuous ROIs ok).
+ * type dtype_in, row steps in BYTES, one per frame (cv::Mat::step of
+ * imagePrev and imageNext; non-continuous ROIs ok, the two may differ).
  * u/v: rows x cols of dtype_out (HSFLOW_F64 = what the reference returns,
  * CV_64FC1, or HSFLOW_F32), row step out_step bytes. */
 int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
-                int rows, int cols, size_t in_step, int window, int iters,
-                double alpha, void *u, void *v, int dtype_out, size_t out_step);
+                int rows, int cols, size_t in_step0, size_t in_step1, int window,
+                int iters, double alpha, void *u, void *v, int dtype_out,
+                size_t out_step);
 
 /* hornSchunck::getGradients (hornSchunck.cpp:19-41): gx, gy, gt. */
 int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
-                     int rows, int cols, size_t in_step, void *gx, void *gy,
-                     void *gt, int dtype_out, size_t out_step);
+                     int rows, int cols, size_t in_step0, size_t in_step1, void *gx,
+                     void *gy, void *gt, int dtype_out, size_t out_step);
 
 /* ---- device pointers, stream-ordered ------------------------------------
  * A batch is `batch` (1..65535) independent frame pairs stored back to back:
  * I0[b][rows][cols], dense (pitch = cols elements), likewise u, v.
  * Inputs are U8, F16 or F32.  Outputs are f32.  `stream` is a hipStream_t (NULL =
- * default stream).  `workspace` is device memory of at least
+ * default stream of the current device); the call runs on the device the
+ * stream belongs to, whatever device is current.  `workspace` is device memory of at least
  * hsflow_workspace_bytes(rows, cols, batch) bytes, 256-byte aligned. */
 size_t hsflow_workspace_bytes(int rows, int cols, int batch);
 
@@ -119,16 +128,15 @@ int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
 int hsflow_set_iters_per_launch(int k);
 int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
 
-/* Kernel of the Jacobi passes: 0 = automatic (default, or HSFLOW_JACOBI),
- * 2 = K2 register tiles, 3 = K3 streaming strips (full passes of even-width
- * images; other passes fall back to K2).  Both give identical bits.
- * Process-wide; not thread-safe against running solves. */
+/* Kernel of the Jacobi passes: 0 = automatic (default), 2 = K2 register
+ * tiles, one launch per pass of iters_per_launch iterations.  Every choice
+ * gives identical bits.  Process-wide; not thread-safe against running
+ * solves. */
 int hsflow_set_jacobi_kernel(int k);
 
 /* Batches of >= 2 pairs are split over up to n side streams (forked from and
  * joined back to the caller's stream with events) so that concurrent Jacobi
- * launches overlap.  1 disables; 0 restores the default (2, or
- * HSFLOW_STREAMS).  Process-wide. */
+ * launches overlap.  1 disables; 0 restores the default (2).  Process-wide. */
 int hsflow_set_max_streams(int n);
 
 /* ---- coarse-to-fine warm start (north_star config 5) ---------------------
@@ -154,9 +162,9 @@ int hsflow_flow_pyramid_device(const void *I0, const void *I1, int dtype_in, int
                                size_t workspace_bytes, void *stream);
 /* Host-buffer, blocking form (same conventions as hsflow_flow). */
 int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
-                        int rows, int cols, size_t in_step, int levels, int window,
-                        int iters, double alpha, void *u, void *v, int dtype_out,
-                        size_t out_step);
+                        int rows, int cols, size_t in_step0, size_t in_step1, int levels,
+                        int window, int iters, double alpha, void *u, void *v,
+                        int dtype_out, size_t out_step);
 
 /* The pyramid's pieces, for callers that schedule the levels themselves
  * (e.g. cpp-optical-flow_amd/row_bands.py, one 8K pair split over GPUs):
@@ -186,11 +194,11 @@ int hsflow_bgr_to_gray_device(const uint8_t *bgr, int rows, int cols, int batch,
                               uint8_t *gray, void *stream);
 
 /* main.cpp:50-51 + :13-14 + :97-98 in one call: two decoded 8-bit BGR frames
- * (row step bgr_step bytes) are uploaded as BGR, converted on the GPU and
- * solved (hornSchunck::getFlow); u/v as in hsflow_flow. */
+ * (row steps bgr_step0, bgr_step1 bytes) are uploaded as BGR, converted on
+ * the GPU and solved (hornSchunck::getFlow); u/v as in hsflow_flow. */
 int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, int rows,
-                    int cols, size_t bgr_step, int window, int iters, double alpha,
-                    void *u, void *v, int dtype_out, size_t out_step);
+                    int cols, size_t bgr_step0, size_t bgr_step1, int window, int iters,
+                    double alpha, void *u, void *v, int dtype_out, size_t out_step);
 
 /* Deterministic synthetic frame pair: I0 = smoothed hash noise
  * around 128 (integer-valued 0..255), I1 = I0's texture shifted by

@@ -13,6 +13,7 @@
 // Link: -lhsflow (cpp-optical-flow_amd/libhsflow.so).
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
@@ -92,11 +93,8 @@ class HornSchunck {
         gradX.resize(n);
         gradY.resize(n);
         gradT.resize(n);
-        Context &c = ctx();
-        c.check(hsflow_gradients(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
-                                 imagePrev.rows, imagePrev.cols, imagePrev.step,
-                                 gradX.data(), gradY.data(), gradT.data(), HSFLOW_F64,
-                                 (size_t)imagePrev.cols * 8));
+        getGradientsInto(imagePrev, imageNext, gradX.data(), gradY.data(), gradT.data(),
+                         HSFLOW_F64, (size_t)imagePrev.cols * 8);
     }
 
     // hornSchunck.cpp:43-75 -> u, v as rows*cols float64 (reallocated, like
@@ -107,30 +105,33 @@ class HornSchunck {
         const size_t n = (size_t)imagePrev.rows * imagePrev.cols;
         u.resize(n);
         v.resize(n);
-        Context &c = ctx();
-        c.check(hsflow_flow(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
-                            imagePrev.rows, imagePrev.cols, imagePrev.step, windowSize,
-                            maxIterations, alpha, u.data(), v.data(), HSFLOW_F64,
-                            (size_t)imagePrev.cols * 8));
+        getFlowInto(imagePrev, imageNext, u.data(), v.data(), HSFLOW_F64,
+                    (size_t)imagePrev.cols * 8);
     }
 
     // Raw form for callers that own output rows (cv::Mat adapter): dtype_out
-    // HSFLOW_F64 or HSFLOW_F32, out_step in bytes.
+    // HSFLOW_F64 or HSFLOW_F32, out_step in bytes.  Each frame keeps its own
+    // row step; frames of different element types are both widened to
+    // float64 first, as hornSchunck.cpp:23-24 converts each with convertTo.
     void getFlowInto(const ImageView &imagePrev, const ImageView &imageNext, void *u,
                      void *v, int dtype_out, size_t out_step) {
         check_pair(imagePrev, imageNext);
+        std::vector<double> ha, hb;
+        const ImageView a = common_type(imagePrev, imageNext, ha);
+        const ImageView b = common_type(imageNext, imagePrev, hb);
         Context &c = ctx();
-        c.check(hsflow_flow(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
-                            imagePrev.rows, imagePrev.cols, imagePrev.step, windowSize,
-                            maxIterations, alpha, u, v, dtype_out, out_step));
+        c.check(hsflow_flow(c.get(), a.data, b.data, a.type, a.rows, a.cols, a.step, b.step,
+                            windowSize, maxIterations, alpha, u, v, dtype_out, out_step));
     }
     void getGradientsInto(const ImageView &imagePrev, const ImageView &imageNext, void *gx,
                           void *gy, void *gt, int dtype_out, size_t out_step) {
         check_pair(imagePrev, imageNext);
+        std::vector<double> ha, hb;
+        const ImageView a = common_type(imagePrev, imageNext, ha);
+        const ImageView b = common_type(imageNext, imagePrev, hb);
         Context &c = ctx();
-        c.check(hsflow_gradients(c.get(), imagePrev.data, imageNext.data, imagePrev.type,
-                                 imagePrev.rows, imagePrev.cols, imagePrev.step, gx, gy, gt,
-                                 dtype_out, out_step));
+        c.check(hsflow_gradients(c.get(), a.data, b.data, a.type, a.rows, a.cols, a.step,
+                                 b.step, gx, gy, gt, dtype_out, out_step));
     }
 
   private:
@@ -145,7 +146,34 @@ class HornSchunck {
         if (!a.data || !b.data) throw Error(HSFLOW_ERR_ARG, "empty image");
         if (a.rows != b.rows || a.cols != b.cols)
             throw Error(HSFLOW_ERR_SIZE, "Image sizes are different");
-        if (a.type != b.type) throw Error(HSFLOW_ERR_ARG, "prev/next element types differ");
+    }
+    static double half_to_double(uint16_t h) {  // IEEE binary16 (CV_16F)
+        const int e = (h >> 10) & 31, f = h & 1023;
+        const double s = (h & 0x8000) ? -1.0 : 1.0;
+        if (e == 0) return s * std::ldexp((double)f, -24);
+        if (e == 31) return f ? std::nan("") : s * HUGE_VAL;
+        return s * std::ldexp((double)(f | 1024), e - 25);
+    }
+    // `m` as it enters the ABI: unchanged when both frames share an element
+    // type, else widened to a dense float64 copy held in `hold`.
+    static ImageView common_type(const ImageView &m, const ImageView &other,
+                                 std::vector<double> &hold) {
+        if (m.type == other.type) return m;
+        hold.resize((size_t)m.rows * m.cols);
+        for (int r = 0; r < m.rows; ++r) {
+            const char *row = (const char *)m.data + (size_t)r * m.step;
+            double *d = hold.data() + (size_t)r * m.cols;
+            for (int c = 0; c < m.cols; ++c) {
+                switch (m.type) {
+                case HSFLOW_U8: d[c] = ((const uint8_t *)row)[c]; break;
+                case HSFLOW_F32: d[c] = ((const float *)row)[c]; break;
+                case HSFLOW_F64: d[c] = ((const double *)row)[c]; break;
+                case HSFLOW_F16: d[c] = half_to_double(((const uint16_t *)row)[c]); break;
+                default: throw Error(HSFLOW_ERR_ARG, "unsupported element type");
+                }
+            }
+        }
+        return {hold.data(), m.rows, m.cols, (size_t)m.cols * 8, HSFLOW_F64};
     }
 };
 

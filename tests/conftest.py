@@ -66,3 +66,10 @@ def norm_rel_err(got, ref):
     ref = np.asarray(ref, np.float64)
     scale = max(float(np.max(np.abs(ref))), 1e-30)
     return float(np.max(np.abs(got - ref))) / scale
+
+
+@pytest.fixture(scope="session")
+def hs():
+    """The product package (cpp-optical-flow_amd/hsflow.py over libhsflow.so)."""
+    import hsflow
+    return hsflow

@@ -40,6 +40,28 @@ int main(int argc, char **argv) {
     hs.getFlow(rp, rn, u, v);
     dump(argv[1], "roi", u, v);
 
+    // ROI prev with a contiguous next: each frame keeps its own row step
+    hs.getFlow(rp, next, u, v);
+    dump(argv[1], "roi_mixed", u, v);
+
+    // frames of different depths (u8 prev, CV_32FC1 next), each converted
+    // on its own as hornSchunck.cpp:23-24 does
+    cv::Mat n32(rows, cols, CV_32FC1);
+    for (int r = 0; r < rows; ++r)
+        for (int c = 0; c < cols; ++c) n32.at<float>(r, c) = b[r * cols + c];
+    hs.getFlow(prev, n32, u, v);
+    dump(argv[1], "mixed_depth", u, v);
+
+    // Output aliasing: u = Mat::zeros(...) and u = uAvg - uUpdateConst
+    // (hornSchunck.cpp:49-50, 72) are MatExpr assignments, which OpenCV
+    // evaluates into the destination with create() -- an existing CV_64FC1
+    // buffer of the right size is written in place, so a header sharing it
+    // sees the result.  The adapter keeps that behaviour.
+    cv::Mat alias = u;
+    hs.getFlow(prev, next, u, v);
+    if (alias.data != u.data) return 11;
+    dump(argv[1], "alias", alias, v);
+
     // CV_16UC1 frames: converted with convertTo(CV_64FC1) (hornSchunck.cpp:23-24)
     cv::Mat p16(rows, cols, CV_16UC1), n16(rows, cols, CV_16UC1);
     for (int r = 0; r < rows; ++r)

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_status_strings():
     L = hsflow.lib()
-    assert L.hsflow_version() == 10000
+    assert L.hsflow_version() == 20000
     assert L.hsflow_status_string(0) == b"ok"
     assert L.hsflow_status_string(-5) == b"image sizes differ"
 
@@ -53,11 +53,11 @@ def test_iters_per_launch_policy():
 
 
 def test_jacobi_kernel_selector():
-    """0 = automatic, 2 = K2 tiles, 3 = K3 streaming strips; others rejected."""
-    for bad in (-1, 1, 4, 99):
+    """0 = automatic, 2 = K2 tiles one launch per pass; others rejected."""
+    for bad in (-1, 1, 3, 99):
         with pytest.raises(hsflow.HsflowError):
             hsflow.set_jacobi_kernel(bad)
-    for k in (2, 3, 0):
+    for k in (2, 0):
         hsflow.set_jacobi_kernel(k)
 
 
@@ -76,7 +76,13 @@ def test_device_entry_points_validate_before_touching_the_gpu():
 
 def test_host_api_rejects_null_context():
     L = hsflow.lib()
-    assert L.hsflow_flow(None, 1, 1, 0, 4, 4, 4, 5, 1, 1.0, 1, 1, 2, 32) == hsflow.HSFLOW_ERR_ARG
+    assert L.hsflow_flow(None, 1, 1, 0, 4, 4, 4, 4, 5, 1, 1.0, 1, 1, 2, 32) == hsflow.HSFLOW_ERR_ARG
+
+
+def test_product_library_ignores_the_environment():
+    """The product libhsflow.so is not the probe build: no HSFLOW_* variable
+    can change what it computes or what a bench times."""
+    assert not hsflow.is_probe_build()
 
 
 def test_bgr_to_gray_matches_reference_conversion():

@@ -42,3 +42,56 @@ def test_bench_prints_one_contract_line():
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert "workload" in d["config"]
+
+
+def test_bench_refuses_diagnostic_environment():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.refuse_diagnostics({"PATH": "/bin", "HSFLOW_BENCH_BACKEND": "gloo"}) == []
+    assert bench.refuse_diagnostics({"HSFLOW_ABLATE": "1", "HSFLOW_STREAMS": "1"}) == \
+        ["HSFLOW_ABLATE", "HSFLOW_STREAMS"]
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")], cwd=ROOT,
+                         env=dict(os.environ, HSFLOW_K2_TL="0"), capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 2 and "HSFLOW_K2_TL" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_parity_check_against_an_oracle_golden():
+    """bench.parity_check: the oracle's own result passes, a 2e-4 relative
+    perturbation of one sampled pixel (or a NaN anywhere) fails."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    import oracle
+    from synth_ref import synth_pair
+    I0, I1 = synth_pair(1000, 40, 64)
+    u, v = oracle.flow(I0, I1, 5, 30, 1.0)
+    e = {"step": 4, "sum_u": float(u.sum()), "sum_v": float(v.sum()),
+         "max_u": float(np.abs(u).max()), "max_v": float(np.abs(v).max())}
+    golden = ("t", e, u[::4, ::4].astype(np.float32), v[::4, ::4].astype(np.float32))
+    ok = bench.parity_check(u.astype(np.float32), v.astype(np.float32), golden)
+    assert ok["ok"] is True and ok["max_rel_err"] < 1e-6
+    bad = u.astype(np.float32).copy()
+    bad[8, 12] += 2e-4 * e["max_u"]
+    assert bench.parity_check(bad, v, golden)["ok"] is False
+    nan = u.astype(np.float32).copy()
+    nan[1, 1] = np.nan
+    assert bench.parity_check(nan, v, golden)["ok"] is False
+    assert bench.parity_check(u, v, None)["ok"] is None
+
+
+def test_bench_golden_fixture_covers_the_bench_workloads():
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    for wl, window in (("1080p", 5), ("4k", 5), ("1080p", 3), ("4k", 3)):
+        w = bench.WORKLOADS[wl]
+        g = bench.golden_entry(w["rows"], w["cols"], w["iters"], window, 1, 1.0)
+        assert g is not None, (wl, window)
+        name, e, us, vs = g
+        step = e["step"]
+        assert us.shape == vs.shape == (-(-w["rows"] // step), -(-w["cols"] // step))
+        assert np.isfinite(us).all() and float(np.abs(us).max()) <= e["max_u"] * (1 + 1e-6)
+        # SURVEY §8d sanity: mean u ~ dx / 8 (Sobel scaling) for dx = +1.5 px
+        assert 0.05 < e["sum_u"] / (w["rows"] * w["cols"]) < 0.3

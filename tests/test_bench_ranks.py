@@ -1,0 +1,95 @@
+"""bench.py's N > 1 code path on CPU: world_size 2 over gloo (the driver runs
+it over RCCL, one process per GPU).  The timing rule (barrier, K timed steps,
+max over ranks) and the config-4 stream leg (rank 0 scatters the pairs,
+each rank solves its share in one batched call, rank 0 gathers) run exactly
+as in bench.py; only the per-batch solver is injected -- the CPU oracle here,
+hsflow.flow_device on the GPU."""
+import os
+import socket
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+ROWS, COLS, ITERS, N_PAIRS = 24, 40, 6, 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _solve_batch(I0, I1):
+    import oracle
+    us, vs = [], []
+    for a, b in zip(I0, I1):
+        u, v = oracle.flow(a.numpy(), b.numpy(), 5, ITERS, 1.0)
+        us.append(torch.from_numpy(u.astype(np.float32)))
+        vs.append(torch.from_numpy(v.astype(np.float32)))
+    return torch.stack(us), torch.stack(vs)
+
+
+def _worker(rank, world, port, q):
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, ROOT, os.path.join(ROOT, "oracle"),
+                    os.path.join(ROOT, "cpp-optical-flow_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        bench.WORKLOADS["tiny"] = dict(rows=ROWS, cols=COLS, iters=ITERS, batch=2)
+        args = types.SimpleNamespace(iters=0, pairs=N_PAIRS, steps=2, window=5, alpha=1.0)
+        dev = torch.device("cpu")
+        # the timing rule: rank 1 is slower, every rank reports the max
+        calls = []
+        el = bench.timed_region(lambda: calls.append(1) or (rank and __import__("time").sleep(0.05)),
+                                lambda: None, 3, 2, world, dev)
+        leg = bench.stream_leg("tiny", args, world, rank, dev, solve_batch=_solve_batch)
+        q.put((rank, len(calls), el, leg))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_n2_timing_and_stream_leg_over_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, ncalls, el, leg = q.get(timeout=240)
+        res[rank] = (ncalls, el, leg)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert res[r][0] == 5, res[r]  # warmup 2 + timed 3
+    # max over ranks: both report the slow rank's time (>= 3 x 50 ms)
+    assert res[0][1] == res[1][1] and res[0][1] >= 0.15
+    leg0, leg1 = res[0][2], res[1][2]
+    assert isinstance(leg0, dict), leg0
+    assert leg0["gathered"] == N_PAIRS and leg0["finite"] and leg0["transport"] == "gloo"
+    assert leg0["pairs_per_s"] == leg1["pairs_per_s"] > 0  # max-over-ranks time
+
+
+def test_stream_leg_gathers_every_pair_in_order_one_rank():
+    """world 1: the same leg without communication returns all pairs."""
+    sys.path[:0] = [ROOT]
+    import bench
+    bench.WORKLOADS["tiny"] = dict(rows=ROWS, cols=COLS, iters=ITERS, batch=2)
+    args = types.SimpleNamespace(iters=0, pairs=3, steps=1, window=5, alpha=1.0)
+    leg = bench.stream_leg("tiny", args, 1, 0, torch.device("cpu"), solve_batch=_solve_batch)
+    assert leg["gathered"] == 3 and leg["finite"] and leg["transport"] == "none (one rank)"

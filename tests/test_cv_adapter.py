@@ -2,8 +2,11 @@
 exact signatures (hornSchunck.cpp:8-75) -- compiled against a cv::Mat test
 double (tests/cpp/cvstub: OpenCV is absent from this image) and run as
 main.cpp:97-98 does.  CPU: it compiles.  GPU: its u, v (CV_64FC1) equal the
-Python host API's bit for bit, for u8, ROI and CV_16U frames; edited public
-fields are honoured; errors surface as cv::Exception."""
+Python host API's bit for bit, for u8, ROI and CV_16U frames, an ROI prev
+with a contiguous next (independent row steps), frames of different depths,
+and an output buffer shared with another header (written in place, as
+OpenCV's MatExpr assignment does); edited public fields are honoured; errors
+surface as cv::Exception."""
 import os
 import subprocess
 
@@ -44,7 +47,7 @@ def test_adapter_matches_host_api(tmp_path):
         return d[:rows * cols].reshape(rows, cols), d[rows * cols:].reshape(rows, cols)
     ctx = hsflow.Context(0)
     ref = ctx.flow(a, b, 5, 100, 1.0)
-    for tag in ("u8", "roi", "u16"):
+    for tag in ("u8", "roi", "u16", "roi_mixed", "mixed_depth", "alias"):
         u, v = load(tag)
         assert np.array_equal(u, ref[0]) and np.array_equal(v, ref[1]), tag
     u, v = load("w3n7")

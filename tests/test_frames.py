@@ -109,6 +109,16 @@ def test_y4m_420_with_frame_parameters(tmp_path):
     assert np.array_equal(src.read(2), lum[2]) and np.array_equal(src.read(1), lum[1])
 
 
+@pytest.mark.parametrize("tag", [b"C420p10", b"C444p12", b"Cmono16", b"C422p10",
+                                 b"C444alpha"])
+def test_y4m_rejects_high_bit_depth_and_alpha(tmp_path, tag):
+    p = str(tmp_path / "hbd.y4m")
+    with open(p, "wb") as f:
+        f.write(b"YUV4MPEG2 W4 H2 F25:1 " + tag + b"\nFRAME\n" + bytes(64))
+    with pytest.raises(fr.FrameError, match="unsupported"):
+        fr.open_source(p)
+
+
 def test_capture_pair_and_consecutive_pairs(tmp_path):
     a = fr.ImageSequence([])
     with pytest.raises(fr.FrameError):
