@@ -24,9 +24,13 @@ Rank 0 prints ONE JSON line.  Besides the driver fields it carries
                 per pixel-iteration x the pixel-iterations of one launch /
                 launch time (> peak is possible: temporal blocking does KB
                 iterations per HBM pass); hbm_frac = PMC bytes per launch
-                (committed profile) / launch time / 8 TB/s; valu_frac = VALU
-                issue cycles / launch cycles from the same profile
-                (DESIGN.md "Roofline")
+                (committed profile of this command, profiles/pmc_*.json) /
+                launch time / 8 TB/s; valu_frac = the launch's VALU
+                instructions per SIMD x the measured cycles per instruction
+                of a SIMD running 4 waves (K2's occupancy; ubench) / launch
+                cycles; step_hbm_frac = the PMC bytes of the timed solve
+                (2 side streams) / ms_per_step / 8 TB/s, the HBM rate the
+                timed region sustains (DESIGN.md "Roofline")
   secondary     the default run also times BASELINE configs[2] (4K x 500 it)
                 with its own roofline and parity check
   pairs_per_s_resident / pairs_per_s_e2e
@@ -58,9 +62,10 @@ WORKLOADS = {
     "8k": dict(rows=4320, cols=7680, iters=1000, batch=1, levels=3, dtype="f16"),
 }
 HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
-VALU_ISSUE_CYCLES = 4.0    # wave64 VALU / v_pk_*_f32 issue cost per SIMD,
-                           # measured in shader cycles (scripts/ubench/valu_tput.hip,
-                           # profiles/r02_valu_tput.txt)
+VALU_CPI_4W = 3.35         # shader cycles per wave64 VALU instruction of a SIMD
+                           # running 4 waves of independent work, K2's mix of
+                           # v_pk_*_f32 (3.42), DPP adds (3.23) and v_add (3.46):
+                           # scripts/ubench/valu_tput.hip, profiles/r02_valu_tput.txt
 SIMDS = 1024               # 256 CUs x 4
 PARITY_TOL = 1e-4          # north_star: 1e-4 relative (norm form)
 GOLDEN_JSON = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
@@ -314,7 +319,7 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
             "algorithmic_B_per_px_iter": 28,
             "compulsory_bytes_per_launch": int(compulsory),
             "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4),
-            "hbm_frac": None, "valu_frac": None}
+            "hbm_frac": None, "valu_frac": None, "step_hbm_frac": None}
     pmc = pmc_for(wl_name, kb, batch) if levels == 1 and window == 5 else None
     if pmc is not None:
         traffic = pmc["hbm_bytes_per_launch"]
@@ -324,9 +329,14 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
         if pmc.get("valu_insts_per_launch") and pmc.get("launch_cycles"):
             # VALU issue cycles per SIMD / the launch's shader cycles (both
             # from the profile; GRBM_GUI_ACTIVE / 8 XCDs = launch cycles)
-            roof["valu_frac"] = round(pmc["valu_insts_per_launch"] * VALU_ISSUE_CYCLES /
+            roof["valu_frac"] = round(pmc["valu_insts_per_launch"] * VALU_CPI_4W /
                                       SIMDS / pmc["launch_cycles"], 4)
             roof["clock_ghz"] = pmc.get("clock_ghz")
+        if pmc.get("step_hbm_bytes_per_pass"):
+            # the timed solve: every pass's PMC bytes over the step time
+            step_bytes = pmc["step_hbm_bytes_per_pass"] * launches_per_solve * batch / pmc["batch"]
+            roof["step_hbm_frac"] = round(step_bytes / (elapsed / args.steps) / 1e9 /
+                                          HBM_PEAK_GBPS, 4)
         roof["pmc_source"] = pmc.get("source")
 
     leg = {"workload": f"{wl_name} {cols}x{rows}, {iters} it"

@@ -44,14 +44,10 @@ namespace {
 
 thread_local std::string g_err;  // errors from calls without a context
 int g_kb_override = 0;
-// Jacobi pass kernel: 0 = automatic, 2 = K2 tiles, one launch per pass
-// (hsflow_set_jacobi_kernel; probe build: HSFLOW_JACOBI sets the default)
-int g_kernel_override = -1;
-
-int jacobi_kernel_choice() {
-    if (g_kernel_override < 0) g_kernel_override = hsflow::probe_env("HSFLOW_JACOBI", 0);
-    return g_kernel_override;
-}
+// Jacobi pass kernel (hsflow_set_jacobi_kernel): 0 = automatic, 2 = K2 tiles,
+// one launch per pass -- both run K2 (the persistent K2p and the streaming
+// K3 alternatives measured slower and were retired)
+int g_kernel_override = 0;
 
 int fail(hsflow_ctx *ctx, int code, const char *fmt, ...) {
     char buf[512];

@@ -1038,6 +1038,15 @@ static hipError_t launch_jacobi_w(JacobiArgs a, int KB, hipStream_t s) {
 // non-integral take the f32-gradient path inside the same launch; the caller
 // must then pick KB with kb_supported(W, KB, true).
 hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s) {
+#ifdef HSFLOW_DEV_W  // kernel development builds: one window (and KB) only
+    if (W != HSFLOW_DEV_W) return hipErrorInvalidValue;
+#ifdef HSFLOW_DEV_KB
+    if (KB != HSFLOW_DEV_KB) return hipErrorInvalidValue;
+    return launch_jacobi_wgv<HSFLOW_DEV_W, HSFLOW_DEV_KB>(a, s);
+#else
+    return launch_jacobi_w<HSFLOW_DEV_W>(a, KB, s);
+#endif
+#else
     switch (W) {
     case 1: return launch_jacobi_w<1>(a, KB, s);
     case 2: return launch_jacobi_w<2>(a, KB, s);
@@ -1055,6 +1064,7 @@ hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s) {
         return hipGetLastError();
     }
     }
+#endif
 }
 
 }  // namespace hsflow

@@ -515,7 +515,8 @@ def set_max_streams(n: int):
 
 
 def set_jacobi_kernel(k: int):
-    """Jacobi pass kernel: 0 = automatic, 2 = K2 tiles, 3 = K3 streaming."""
+    """Jacobi pass kernel: 0 = automatic, 2 = K2 tiles, one launch per pass
+    (both run K2 today; include/hsflow.h)."""
     _check(lib().hsflow_set_jacobi_kernel(int(k)))
 
 
