@@ -250,7 +250,10 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
             stream.wait_stream(cap)
             torch.cuda.synchronize(dev)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            # thread_local: only this thread's calls can invalidate the
+            # capture (the secondary leg captures after the process group,
+            # whose watchdog thread polls events, is up)
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 solve(torch.cuda.current_stream(dev))
             torch.cuda.synchronize(dev)
         except Exception as e:  # pragma: no cover - eager fallback, reported
