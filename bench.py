@@ -62,6 +62,7 @@ WORKLOADS = {
     "8k": dict(rows=4320, cols=7680, iters=1000, batch=1, levels=3, dtype="f16"),
 }
 HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+COPY_PEAK_GBPS = 6290.0    # MI355X_MICROARCH.md: float4 copy, measured (79 % of spec)
 VALU_CPI_4W = 3.35         # shader cycles per wave64 VALU instruction of a SIMD
                            # running 4 waves of independent work, K2's mix of
                            # v_pk_*_f32 (3.42), DPP adds (3.23) and v_add (3.46):
@@ -99,6 +100,8 @@ def parse(argv=None):
                     help="time eager solves instead of hipGraph replays of one solve")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the configs[2] (4K) block of the default run")
+    ap.add_argument("--no-w3", action="store_true",
+                    help="skip the window-3 block of the default run (SURVEY §8d)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pairs/s leg")
     ap.add_argument("--no-stream", action="store_true", help="skip the config-4 stream leg")
     ap.add_argument("--mode", choices=["resident", "stream", "bands"], default="resident",
@@ -200,7 +203,8 @@ def pmc_for(workload, kb, batch):
 
 
 # --------------------------------------------------------------- resident
-def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False):
+def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False,
+                 window=None):
     """One workload, inputs resident in HBM: a step is one full solve of
     `batch` pairs per rank (hipGraph replay).  Returns the leg's dict."""
     import numpy as np
@@ -213,7 +217,7 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
     batch = args.batch or wl["batch"]
     levels = args.levels or wl.get("levels", 1)
     in_dtype = args.dtype or wl.get("dtype", "f32")
-    window, alpha = args.window, args.alpha
+    window, alpha = (window or args.window), args.alpha
 
     # synthetic pairs, seed 1000 + global pair index
     np_dtype = np.uint8 if in_dtype == "u8" else np.float32
@@ -354,6 +358,29 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
     del I0, I1, u, v, ws, pws, graph
     torch.cuda.empty_cache()
     return leg
+
+
+def hbm_stream_peak(dev, nbytes=2 << 30, reps=5):
+    """Measured device copy rate (read + write bytes per second, GB/s) of a
+    2 GiB buffer, far past the 256 MB Infinity Cache: the practical HBM
+    ceiling the roofline is also quoted against."""
+    import torch
+    n = nbytes // 4
+    a = torch.empty(n, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbps = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbps, 1)
 
 
 # --------------------------------------------------------------- e2e
@@ -539,6 +566,11 @@ def main():
     sec = None
     if default_run and not args.no_secondary:
         sec = resident_leg("4k", args, dev, world, rank)
+    w3 = None
+    if default_run and not args.no_w3:
+        # windowSize 5 is the headline, report 3 (north_star) too
+        w3 = resident_leg("1080p", args, dev, world, rank, window=3)
+    stream_peak = hbm_stream_peak(dev) if rank == 0 else None
     e2e = None
     if not args.no_e2e and args.workload != "8k" and rank == 0:
         e2e = e2e_leg(args.workload, args, dev)
@@ -590,10 +622,27 @@ def main():
                                                      "pairs_per_s_resident", "roofline",
                                                      "parity")}
             line["secondary"]["unit"] = "Mpix*iter/s"
+        if w3 is not None:
+            line["window3"] = {k: w3[k] for k in ("workload", "value", "ms_per_step",
+                                                  "pairs_per_s_resident", "parity")}
+            line["window3"]["unit"] = "Mpix*iter/s"
+            line["window3"]["avg_launch_ms"] = w3["roofline"]["avg_launch_ms"]
+        if stream_peak is not None:
+            # also against a measured stream-copy peak -- the
+            # guide's float4 copy (6.29 TB/s, the higher and so stricter
+            # one) next to torch's copy_ measured here
+            for leg in (line["roofline"], line.get("secondary", {}).get("roofline")):
+                if leg is not None:
+                    leg["copy_peak_gbps"] = COPY_PEAK_GBPS
+                    leg["torch_copy_gbps"] = stream_peak
+                    if leg.get("traffic"):
+                        leg["hbm_frac_vs_copy_peak"] = round(
+                            leg["traffic"] / (leg["avg_launch_ms"] * 1e-3) / 1e9 /
+                            max(COPY_PEAK_GBPS, stream_peak), 4)
         if strm is not None:
             line["stream"] = strm
         print(json.dumps(line), flush=True)
-        for leg in (prim, sec):
+        for leg in (prim, sec, w3):
             if leg is not None and leg["parity"] is not None and leg["parity"]["ok"] is False:
                 print(f"bench: PARITY FAILURE on {leg['workload']}: {leg['parity']}",
                       file=sys.stderr)
