@@ -764,6 +764,56 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     return HSFLOW_OK;
 }
 
+// Frame-parallel host API over several GPUs of the node from ONE process
+// (include/hsflow.h): one host thread, context and stream per listed device,
+// pair j on devices[j % n].  The per-pair work is exactly hsflow_flow.
+int hsflow_flow_multi(const int *devices, int n_devices, int batch,
+                      const void *const *I0, const void *const *I1, int dtype_in, int rows,
+                      int cols, size_t in_step0, size_t in_step1, int window, int iters,
+                      double alpha, void *const *u, void *const *v, int dtype_out,
+                      size_t out_step) {
+    if (!devices || n_devices < 1 || n_devices > 64)
+        return fail(nullptr, HSFLOW_ERR_ARG, "need 1..64 devices, got %d", n_devices);
+    if (batch < 0) return fail(nullptr, HSFLOW_ERR_ARG, "batch %d < 0", batch);
+    if (batch == 0) return HSFLOW_OK;
+    if (!I0 || !I1 || !u || !v) return fail(nullptr, HSFLOW_ERR_ARG, "null pair array");
+    for (int j = 0; j < batch; ++j)
+        if (!I0[j] || !I1[j] || !u[j] || !v[j])
+            return fail(nullptr, HSFLOW_ERR_ARG, "null buffer in pair %d", j);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(nullptr, HSFLOW_ERR_NODEV, "no HIP device");
+    for (int k = 0; k < n_devices; ++k)
+        if (devices[k] < 0 || devices[k] >= ndev)
+            return fail(nullptr, HSFLOW_ERR_NODEV, "device %d of %d", devices[k], ndev);
+    const int nw = std::min(n_devices, batch);
+    std::vector<int> rc(nw, HSFLOW_OK);
+    std::vector<std::string> msg(nw);
+    std::vector<std::thread> pool;
+    pool.reserve(nw);
+    for (int k = 0; k < nw; ++k) {
+        pool.emplace_back([&, k] {
+            hsflow_ctx *ctx = nullptr;
+            int r = hsflow_create(&ctx, devices[k]);
+            if (r) {
+                rc[k] = r;
+                msg[k] = hsflow_last_error(nullptr);  // this worker's message
+                return;
+            }
+            for (int j = k; j < batch && r == HSFLOW_OK; j += nw)
+                r = hsflow_flow(ctx, I0[j], I1[j], dtype_in, rows, cols, in_step0, in_step1,
+                                window, iters, alpha, u[j], v[j], dtype_out, out_step);
+            if (r) msg[k] = hsflow_last_error(ctx);
+            hsflow_destroy(ctx);
+            rc[k] = r;
+        });
+    }
+    for (auto &t : pool) t.join();
+    for (int k = 0; k < nw; ++k)
+        if (rc[k]) return fail(nullptr, rc[k], "device %d: %s", devices[k], msg[k].c_str());
+    return HSFLOW_OK;
+}
+
 int hsflow_pyramid_level_size(int rows, int cols, int level, int *level_rows,
                               int *level_cols) {
     if (rows < 1 || cols < 1 || level < 0 || level >= HSFLOW_MAX_LEVELS) return HSFLOW_ERR_ARG;

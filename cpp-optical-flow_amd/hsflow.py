@@ -50,7 +50,7 @@ EXPORTS = (
     "hsflow_pyramid_level_size", "hsflow_pyramid_workspace_bytes",
     "hsflow_flow_pyramid_device", "hsflow_flow_pyramid", "hsflow_bgr_to_gray_device",
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
-    "hsflow_set_jacobi_kernel", "hsflow_build_flags",
+    "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
 )
 BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
 
@@ -127,6 +127,10 @@ def lib():
                                   _vp, _vp, i, _sz]
     L.hsflow_bgr_to_gray.argtypes = [_vp, i, i, _sz, _vp, _sz]
     L.hsflow_synth_pair.argtypes = [ctypes.c_uint64, i, i, i, i, _vp, _vp, _vp, _vp]
+    L.hsflow_flow_multi.argtypes = [ctypes.POINTER(i), i, i, ctypes.POINTER(_vp),
+                                    ctypes.POINTER(_vp), i, i, i, _sz, _sz, i, i,
+                                    ctypes.c_double, ctypes.POINTER(_vp),
+                                    ctypes.POINTER(_vp), i, _sz]
     _lib = L
     return L
 
@@ -273,6 +277,37 @@ class Context:
 
 
 _default_ctx = None
+
+
+def flow_multi(devices, pairs, window: int, iters: int, alpha: float,
+               out_dtype=np.float64):
+    """Frame-parallel getFlow of host pairs over several GPUs from one
+    process (hsflow_flow_multi): pair j on devices[j % len(devices)], one
+    host thread + context per listed device.  `pairs`: list of (I0, I1)
+    arrays of one shape and dtype.  Returns [(u, v), ...] in pair order."""
+    pairs = [(_as_image(a), _as_image(b)) for a, b in pairs]
+    if not pairs:
+        return []
+    rows, cols = pairs[0][0].shape
+    dt, st0, st1 = pairs[0][0].dtype, pairs[0][0].strides[0], pairs[0][1].strides[0]
+    for a, b in pairs:
+        if a.shape != (rows, cols) or b.shape != (rows, cols):
+            raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
+        if a.dtype != dt or b.dtype != dt or a.strides[0] != st0 or b.strides[0] != st1:
+            raise HsflowError(HSFLOW_ERR_ARG, "pairs must share dtype and row steps")
+    out = [(np.empty((rows, cols), out_dtype), np.empty((rows, cols), out_dtype))
+           for _ in pairs]
+    n = len(pairs)
+    P = _vp * n
+    devs = (ctypes.c_int * len(devices))(*devices)
+    rc = lib().hsflow_flow_multi(
+        devs, len(devices), n, P(*[a.ctypes.data for a, _ in pairs]),
+        P(*[b.ctypes.data for _, b in pairs]), _dtype_code(pairs[0][0]), rows, cols, st0,
+        st1, int(window), int(iters), float(alpha), P(*[u.ctypes.data for u, _ in out]),
+        P(*[v.ctypes.data for _, v in out]), F64 if out_dtype == np.float64 else F32,
+        out[0][0].strides[0])
+    _check(rc)
+    return out
 
 
 def default_context() -> Context:

@@ -91,6 +91,21 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
                 int iters, double alpha, void *u, void *v, int dtype_out,
                 size_t out_step);
 
+/* Frame-parallel getFlow over several GPUs of this node from ONE process,
+ * for C/C++ callers that do not run one process per GPU (the multi-rank
+ * form is cpp-optical-flow_amd/frame_parallel.py over torch.distributed).
+ * Pair j -- host frames I0[j], I1[j] (rows x cols, dtype_in, row steps
+ * in_step0 / in_step1), host outputs u[j], v[j] (dtype_out, out_step) -- is
+ * solved on devices[j % n_devices], each listed device by its own host
+ * thread, context and stream, exactly as hsflow_flow (same bits).  A device
+ * may be listed twice (two streams on one GPU).  Blocking; returns the
+ * first error, its message in hsflow_last_error(NULL). */
+int hsflow_flow_multi(const int *devices, int n_devices, int batch,
+                      const void *const *I0, const void *const *I1, int dtype_in, int rows,
+                      int cols, size_t in_step0, size_t in_step1, int window, int iters,
+                      double alpha, void *const *u, void *const *v, int dtype_out,
+                      size_t out_step);
+
 /* hornSchunck::getGradients (hornSchunck.cpp:19-41): gx, gy, gt. */
 int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
                      int rows, int cols, size_t in_step0, size_t in_step1, void *gx,

@@ -183,4 +183,39 @@ inline void compute(const ImageView &I0, const ImageView &I1, double alpha, int 
     HornSchunck(windowSize, nIter, alpha).getFlow(I0, I1, u, v);
 }
 
+// Frame-parallel getFlow over several GPUs from one process
+// (hsflow_flow_multi): pair j (prev[j], next[j], all one size, type and row
+// steps) on devices[j % devices.size()]; u[j], v[j] receive CV_64FC1-style
+// rows x cols doubles (resized here).
+inline void flowMulti(const std::vector<int> &devices, const std::vector<ImageView> &prev,
+                      const std::vector<ImageView> &next, int windowSize, int maxIterations,
+                      double alpha, std::vector<std::vector<double>> &u,
+                      std::vector<std::vector<double>> &v) {
+    if (prev.size() != next.size()) throw Error(HSFLOW_ERR_ARG, "prev/next counts differ");
+    const size_t n = prev.size();
+    u.resize(n);
+    v.resize(n);
+    if (n == 0) return;
+    const ImageView &a = prev[0], &b = next[0];
+    std::vector<const void *> I0(n), I1(n);
+    std::vector<void *> pu(n), pv(n);
+    for (size_t j = 0; j < n; ++j) {
+        if (prev[j].rows != a.rows || prev[j].cols != a.cols || prev[j].type != a.type ||
+            prev[j].step != a.step || next[j].rows != a.rows || next[j].cols != a.cols ||
+            next[j].type != a.type || next[j].step != b.step)
+            throw Error(HSFLOW_ERR_SIZE, "pairs differ in size, type or row step");
+        I0[j] = prev[j].data;
+        I1[j] = next[j].data;
+        u[j].assign((size_t)a.rows * a.cols, 0.0);
+        v[j].assign((size_t)a.rows * a.cols, 0.0);
+        pu[j] = u[j].data();
+        pv[j] = v[j].data();
+    }
+    const int rc = hsflow_flow_multi(devices.data(), (int)devices.size(), (int)n, I0.data(),
+                                     I1.data(), a.type, a.rows, a.cols, a.step, b.step,
+                                     windowSize, maxIterations, alpha, pu.data(), pv.data(),
+                                     HSFLOW_F64, (size_t)a.cols * sizeof(double));
+    if (rc != HSFLOW_OK) throw Error(rc, hsflow_last_error(nullptr));
+}
+
 }  // namespace hsflow

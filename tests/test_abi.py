@@ -1,6 +1,7 @@
 """CPU tests of the C-ABI library: it loads, exports every symbol declared in
 include/hsflow.h, validates arguments, and its host utilities are exact.
 No GPU compute here."""
+import ctypes
 import os
 import re
 
@@ -72,6 +73,27 @@ def test_device_entry_points_validate_before_touching_the_gpu():
                                   None) == hsflow.HSFLOW_ERR_ARG  # workspace too small
     assert L.hsflow_gradients_device(1, 1, 2, 10, 10, 1, None, None, None, 1, 10 ** 6,
                                      None) == hsflow.HSFLOW_ERR_ARG  # F64 on device
+
+
+def test_flow_multi_validates_before_touching_the_gpu():
+    """hsflow_flow_multi (one process, several GPUs): bad device lists and
+    null pair buffers are rejected on the host; an empty batch is a no-op."""
+    L = hsflow.lib()
+    i = ctypes.c_int
+    P = ctypes.c_void_p * 1
+    devs = (i * 1)(0)
+    one = P(None)
+    assert L.hsflow_flow_multi(devs, 0, 1, one, one, 0, 4, 4, 4, 4, 5, 1, 1.0, one, one,
+                               2, 32) == hsflow.HSFLOW_ERR_ARG           # no devices
+    assert L.hsflow_flow_multi(None, 1, 1, one, one, 0, 4, 4, 4, 4, 5, 1, 1.0, one, one,
+                               2, 32) == hsflow.HSFLOW_ERR_ARG
+    assert L.hsflow_flow_multi(devs, 1, 1, one, one, 0, 4, 4, 4, 4, 5, 1, 1.0, one, one,
+                               2, 32) == hsflow.HSFLOW_ERR_ARG           # null frames
+    assert "pair 0" in L.hsflow_last_error(None).decode()
+    assert L.hsflow_flow_multi(devs, 1, 0, None, None, 0, 4, 4, 4, 4, 5, 1, 1.0, None,
+                               None, 2, 32) == hsflow.HSFLOW_OK          # empty batch
+    assert L.hsflow_flow_multi(devs, 1, -1, None, None, 0, 4, 4, 4, 4, 5, 1, 1.0, None,
+                               None, 2, 32) == hsflow.HSFLOW_ERR_ARG
 
 
 def test_host_api_rejects_null_context():

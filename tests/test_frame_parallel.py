@@ -150,3 +150,34 @@ def test_frame_parallel_gpu_solver_world2_bit_identical():
     for j, (I0, I1) in enumerate(_gpu_stream()):
         u, v = _gpu_solve(I0, I1)
         assert np.array_equal(flows[j][0], u.numpy()) and np.array_equal(flows[j][1], v.numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_flow_multi_equals_single_context_bits(devices):
+    """hsflow_flow_multi (C/C++ callers, one process, pair j on
+    devices[j % n], one host thread + context per listed device; the box
+    has one GPU, so the same device is listed up to 3 times = concurrent
+    contexts) gives every pair exactly the single-context getFlow bits, in
+    pair order, u8 and f32 frames, CV_64FC1 and f32 outputs."""
+    import hsflow
+    rows, cols = 120, 200
+    for dtype, out in ((np.uint8, np.float64), (np.float32, np.float32)):
+        pairs = [hsflow.synth_pair(2000 + j, rows, cols, dtype=dtype) for j in range(5)]
+        got = hsflow.flow_multi(devices, pairs, 5, 40, 1.0, out_dtype=out)
+        ctx = hsflow.Context(0)
+        try:
+            for (a, b), (u, v) in zip(pairs, got):
+                ur, vr = ctx.flow(a, b, 5, 40, 1.0, out_dtype=out)
+                assert np.array_equal(u, ur) and np.array_equal(v, vr)
+        finally:
+            ctx.close()
+
+
+@pytest.mark.gpu
+def test_flow_multi_reports_a_bad_device():
+    import hsflow
+    a, b = hsflow.synth_pair(1, 16, 16)
+    with pytest.raises(hsflow.HsflowError) as e:
+        hsflow.flow_multi([0, 99], [(a, b), (a, b)], 5, 1, 1.0)
+    assert e.value.status == hsflow.HSFLOW_ERR_NODEV
