@@ -383,6 +383,37 @@ def hbm_stream_peak(dev, nbytes=2 << 30, reps=5):
     return round(gbps, 1)
 
 
+def config1_leg(dev, reps=20):
+    """BASELINE configs[0]: the KITTI 000050 centre
+    crop, 256x256 u8, ws 5, alpha 1, 100 iterations -- the reference's own
+    CPU-runnable case.  GPU: the host-buffer getFlow path (hsflow_flow:
+    upload, solve, CV_64FC1 download), median of `reps`; parity against the
+    committed golden (u, v) of the crop (tests/golden/crop256.npz, pinned by
+    the reference's plots); CPU: the float64 port on 1 thread."""
+    import numpy as np
+    import hsflow
+    z = np.load(os.path.join(ROOT, "tests", "golden", "crop256.npz"))
+    I0, I1 = z["I0"], z["I1"]
+    hs = hsflow.hornSchunck(5, 100, 1.0)
+    u, v = hs.getFlow(I0, I1)  # warm
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        u, v = hs.getFlow(I0, I1)
+        ts.append(time.perf_counter() - t)
+    ms = sorted(ts)[len(ts) // 2] * 1e3
+    err = max(float(np.max(np.abs(u - z["u"]))) / float(np.max(np.abs(z["u"]))),
+              float(np.max(np.abs(v - z["v"]))) / float(np.max(np.abs(z["v"]))))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    t = time.perf_counter()
+    oracle.flow(I0.astype(np.float64), I1.astype(np.float64), 5, 100, 1.0, nthreads=1)
+    cpu_ms = (time.perf_counter() - t) * 1e3
+    return {"workload": "KITTI 000050 crop 256x256 u8, ws 5, alpha 1, 100 it",
+            "gpu_ms_host_api": round(ms, 3), "cpu_port_ms_1_thread": round(cpu_ms, 1),
+            "parity": {"golden": "crop256", "max_rel_err": err, "ok": bool(err <= PARITY_TOL)}}
+
+
 # --------------------------------------------------------------- e2e
 def e2e_leg(wl_name, args, dev, n_batches=6):
     """End-to-end pairs/s as BASELINE.md defines it: pinned host u8 gray
@@ -578,6 +609,7 @@ def main():
     if not args.no_stream and args.workload == "1080p":
         strm = stream_leg("1080p", args, world, rank, dev)
 
+    c1 = config1_leg(dev) if (default_run and rank == 0) else None
     cpu = cpu_all = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(prim["rows"], prim["cols"], args.window, args.alpha,
@@ -587,6 +619,10 @@ def main():
         n_thr = min(16, os.cpu_count() or 1)
         cpu_all = cpu_baseline(prim["rows"], prim["cols"], args.window, args.alpha,
                                args.cpu_iters, n_thr)
+        if sec is not None:
+            # the CPU line per config -- 4K on 1 thread, bounded
+            sec["cpu_baseline"] = cpu_baseline(sec["rows"], sec["cols"], args.window,
+                                               args.alpha, args.cpu_iters or 20)
 
     status = 0
     if rank == 0:
@@ -620,8 +656,10 @@ def main():
         if sec is not None:
             line["secondary"] = {k: sec[k] for k in ("workload", "value", "ms_per_step",
                                                      "pairs_per_s_resident", "roofline",
-                                                     "parity")}
+                                                     "parity", "cpu_baseline") if k in sec}
             line["secondary"]["unit"] = "Mpix*iter/s"
+        if c1 is not None:
+            line["config1"] = c1
         if w3 is not None:
             line["window3"] = {k: w3[k] for k in ("workload", "value", "ms_per_step",
                                                   "pairs_per_s_resident", "parity")}
@@ -642,7 +680,7 @@ def main():
         if strm is not None:
             line["stream"] = strm
         print(json.dumps(line), flush=True)
-        for leg in (prim, sec, w3):
+        for leg in (prim, sec, w3, c1):
             if leg is not None and leg["parity"] is not None and leg["parity"]["ok"] is False:
                 print(f"bench: PARITY FAILURE on {leg['workload']}: {leg['parity']}",
                       file=sys.stderr)
