@@ -415,11 +415,15 @@ def config1_leg(dev, reps=20):
 
 
 # --------------------------------------------------------------- e2e
-def e2e_leg(wl_name, args, dev, n_batches=6):
+def e2e_leg(wl_name, args, dev, n_batches=12):
     """End-to-end pairs/s as BASELINE.md defines it: pinned host u8 gray
     frames (what main.cpp:13-14 hands over) -> H2D -> K1 + K2 -> D2H of u, v
     (f32), batch after batch.  Copies run on their own streams and overlap
-    the neighbouring batches' solves (double-buffered device slots)."""
+    the neighbouring batches' solves (double-buffered device slots).  The
+    downloads go through hsflow_download_device (the runtime's DMA engines):
+    torch's copy_ into pinned memory runs as a 256-workgroup blit kernel per
+    plane that takes the next batch's Jacobi workgroup slots (1275 vs ~1600
+    pairs/s; scripts/e2e_probe.py, scripts/pcie/d2h_engine_probe.hip)."""
     import numpy as np
     import torch
     import hsflow
@@ -444,6 +448,32 @@ def e2e_leg(wl_name, args, dev, n_batches=6):
     ev = {k: [torch.cuda.Event() for _ in range(2)]
           for k in ("in", "done", "in_free", "out_free")}
 
+    def solve(sl, s):
+        hsflow.flow_device(d_in[sl][0], d_in[sl][1], args.window, iters, args.alpha,
+                           d_out[sl][0], d_out[sl][1], ws[sl], s)
+
+    # each slot's solve is one hipGraph, as in the resident leg: eager, the
+    # ~100 dependent launches of a solve leave dispatch gaps on the GPU
+    graphs = [None, None]
+    if not args.no_graph:
+        try:
+            cur = torch.cuda.current_stream(dev)
+            for sl in range(2):
+                cap = torch.cuda.Stream(dev)
+                cap.wait_stream(cur)
+                with torch.cuda.stream(cap):
+                    solve(sl, cap)  # eager once: library side streams exist
+                cur.wait_stream(cap)
+                torch.cuda.synchronize(dev)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    solve(sl, torch.cuda.current_stream(dev))
+                graphs[sl] = g
+            torch.cuda.synchronize(dev)
+        except Exception as e:  # pragma: no cover - eager fallback, reported
+            print(f"bench: e2e graph capture failed ({e}); eager solves", file=sys.stderr)
+            graphs = [None, None]
+
     def run(n):
         for k in range(n):
             sl = k % 2
@@ -458,14 +488,16 @@ def e2e_leg(wl_name, args, dev, n_batches=6):
                 s_cmp.wait_event(ev["in"][sl])
                 if k >= 2:
                     s_cmp.wait_event(ev["out_free"][sl])
-                hsflow.flow_device(d_in[sl][0], d_in[sl][1], args.window, iters, args.alpha,
-                                   d_out[sl][0], d_out[sl][1], ws[sl], s_cmp)
+                if graphs[sl] is not None:
+                    graphs[sl].replay()  # on s_cmp, the current stream
+                else:
+                    solve(sl, s_cmp)
                 ev["in_free"][sl].record(s_cmp)
                 ev["done"][sl].record(s_cmp)
             with torch.cuda.stream(s_d2h):
                 s_d2h.wait_event(ev["done"][sl])
-                h_out[sl][0].copy_(d_out[sl][0], non_blocking=True)
-                h_out[sl][1].copy_(d_out[sl][1], non_blocking=True)
+                hsflow.download_device(h_out[sl][0], d_out[sl][0], s_d2h)
+                hsflow.download_device(h_out[sl][1], d_out[sl][1], s_d2h)
                 ev["out_free"][sl].record(s_d2h)
         torch.cuda.synchronize(dev)
 
@@ -473,11 +505,17 @@ def e2e_leg(wl_name, args, dev, n_batches=6):
     t = time.perf_counter()
     run(n_batches)
     dt = time.perf_counter() - t
-    ok = bool(torch.isfinite(h_out[0][0]).all())
+    # the last batch's flow arrived intact on the host
+    last = (n_batches - 1) % 2
+    ok = bool(torch.isfinite(h_out[last][0]).all()) and \
+        bool(torch.equal(h_out[last][0], d_out[last][0].cpu())) and \
+        bool(torch.equal(h_out[last][1], d_out[last][1].cpu()))
     return {"pairs_per_s_e2e": round(n_batches * batch / dt, 2),
             "e2e": {"workload": f"{wl_name}, {batch} pairs per batch, {n_batches} batches",
                     "input": "pinned host u8 gray frames", "output": "pinned host f32 u, v",
-                    "ms_per_batch": round(dt / n_batches * 1e3, 3), "finite": ok}}
+                    "ms_per_batch": round(dt / n_batches * 1e3, 3),
+                    "solve": "hipGraph replay" if graphs[0] is not None else "eager",
+                    "finite": ok}}
 
 
 # --------------------------------------------------------------- stream

@@ -933,6 +933,27 @@ int hsflow_bgr_to_gray_device(const uint8_t *bgr, int rows, int cols, int batch,
     return HSFLOW_OK;
 }
 
+int hsflow_download_device(void *dst, const void *src, size_t bytes, void *stream) {
+    if (bytes == 0) return HSFLOW_OK;
+    if (!dst || !src) return fail(nullptr, HSFLOW_ERR_ARG, "null pointer");
+    DeviceGuard g((hipStream_t)stream);
+    // As a pitched copy the runtime moves a device -> pinned host download
+    // with its DMA engines at ~46 GB/s (a flat hipMemcpyAsync: ~29 GB/s;
+    // torch's copy_ of pinned memory: a blit kernel that takes the Jacobi
+    // passes' workgroup slots; scripts/pcie/d2h_engine_probe.hip).
+    constexpr size_t kRow = 7680;  // bytes per pitched row
+    const size_t rows = bytes / kRow, tail = bytes - rows * kRow;
+    hipStream_t s = (hipStream_t)stream;
+    if (rows > 0)
+        HIP_TRY(nullptr, hipMemcpy2DAsync(dst, kRow, src, kRow, kRow, rows,
+                                          hipMemcpyDeviceToHost, s));
+    if (tail > 0)
+        HIP_TRY(nullptr, hipMemcpyAsync((char *)dst + rows * kRow,
+                                        (const char *)src + rows * kRow, tail,
+                                        hipMemcpyDeviceToHost, s));
+    return HSFLOW_OK;
+}
+
 int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, int rows,
                     int cols, size_t bgr_step0, size_t bgr_step1, int window, int iters,
                     double alpha, void *u, void *v, int dtype_out, size_t out_step) {

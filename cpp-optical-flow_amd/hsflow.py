@@ -51,6 +51,7 @@ EXPORTS = (
     "hsflow_flow_pyramid_device", "hsflow_flow_pyramid", "hsflow_bgr_to_gray_device",
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
     "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
+    "hsflow_download_device",
 )
 BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
 
@@ -127,6 +128,7 @@ def lib():
                                   _vp, _vp, i, _sz]
     L.hsflow_bgr_to_gray.argtypes = [_vp, i, i, _sz, _vp, _sz]
     L.hsflow_synth_pair.argtypes = [ctypes.c_uint64, i, i, i, i, _vp, _vp, _vp, _vp]
+    L.hsflow_download_device.argtypes = [_vp, _vp, _sz, _vp]
     L.hsflow_flow_multi.argtypes = [ctypes.POINTER(i), i, i, ctypes.POINTER(_vp),
                                     ctypes.POINTER(_vp), i, i, i, _sz, _sz, i, i,
                                     ctypes.c_double, ctypes.POINTER(_vp),
@@ -277,6 +279,21 @@ class Context:
 
 
 _default_ctx = None
+
+
+def download_device(dst, src, stream=None):
+    """Stream-ordered download of the CUDA tensor `src` into the pinned host
+    tensor `dst` (same byte size) through the runtime's DMA engines
+    (hsflow_download_device), so it overlaps Jacobi passes running on other
+    streams; torch's own copy_ of pinned memory runs as a blit kernel that
+    takes their workgroup slots."""
+    if src.numel() * src.element_size() != dst.numel() * dst.element_size():
+        raise HsflowError(HSFLOW_ERR_ARG, "download sizes differ")
+    if not (src.is_contiguous() and dst.is_contiguous()):
+        raise HsflowError(HSFLOW_ERR_ARG, "download tensors must be contiguous")
+    _check(lib().hsflow_download_device(dst.data_ptr(), src.data_ptr(),
+                                        src.numel() * src.element_size(),
+                                        _stream_ptr(stream, src.device)))
 
 
 def flow_multi(devices, pairs, window: int, iters: int, alpha: float,

@@ -154,6 +154,14 @@ int hsflow_set_jacobi_kernel(int k);
  * launches overlap.  1 disables; 0 restores the default (2).  Process-wide. */
 int hsflow_set_max_streams(int n);
 
+/* Stream-ordered download of `bytes` from device memory to pinned host
+ * memory (hipHostMalloc / torch pin_memory), issued so the runtime moves it
+ * with its DMA engines (~46 GB/s over PCIe Gen5) instead of a blit kernel:
+ * a download of batch k then overlaps the Jacobi passes of batch k+1 on
+ * other streams without taking their workgroup slots (main.cpp:99-104
+ * consumes u, v on the host). */
+int hsflow_download_device(void *dst, const void *src, size_t bytes, void *stream);
+
 /* ---- coarse-to-fine warm start (north_star config 5) ---------------------
  * The reference's HS has no pyramid; the repository's own multi-resolution
  * code is the precedent (BMOpticalFlow/.../OpticalFlow/MultiResolution.cpp:

@@ -96,6 +96,15 @@ def test_flow_multi_validates_before_touching_the_gpu():
                                None, 2, 32) == hsflow.HSFLOW_ERR_ARG
 
 
+def test_download_device_validates_on_the_host():
+    """hsflow_download_device: zero bytes is a no-op, null buffers are
+    rejected before any runtime call."""
+    L = hsflow.lib()
+    assert L.hsflow_download_device(None, None, 0, None) == hsflow.HSFLOW_OK
+    assert L.hsflow_download_device(None, 1, 8, None) == hsflow.HSFLOW_ERR_ARG
+    assert L.hsflow_download_device(1, None, 8, None) == hsflow.HSFLOW_ERR_ARG
+
+
 def test_host_api_rejects_null_context():
     L = hsflow.lib()
     assert L.hsflow_flow(None, 1, 1, 0, 4, 4, 4, 4, 5, 1, 1.0, 1, 1, 2, 32) == hsflow.HSFLOW_ERR_ARG
