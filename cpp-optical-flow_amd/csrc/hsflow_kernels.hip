@@ -512,7 +512,11 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
 
     constexpr int kOOB = 0x7FFFFFF0;
     const int ablate = kProbeBuild ? p.ablate : 0;  // compiled out of the product
+#ifdef HSFLOW_DEV_NOMEM  // development ablation: loads and stores out of range
+    const int nbytes = 0;
+#else
     const int nbytes = ablate == 2 ? 0 : plane_bytes;
+#endif
     const auto u_rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase), 0, p.u_in ? nbytes : 0,
         0x00020000);
@@ -616,7 +620,11 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         hv = f2v{c, d};
     };
 
+#ifdef HSFLOW_DEV_NOIT  // development ablation: no iterations
+    const int n_it = 0 * p.iters;
+#else
     const int n_it = ablate == 1 ? 0 : p.iters;
+#endif
     // The vertical sums follow the parity of the image row (PAR = parity
     // of slab row 0), so every slab height, blocking depth and kernel
     // adds in the same order.  w = 5: pair sums Q(t) = h(t) + h(t+1) at
@@ -644,7 +652,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
             xch[par][wv][AR + k][0][lane] = make_float2(hbu[k].x, hbu[k].y);
             xch[par][wv][AR + k][1][lane] = make_float2(hbv[k].x, hbv[k].y);
         }
+#ifndef HSFLOW_DEV_NOBAR  // development ablation: timing without the barriers
         __syncthreads();
+#endif
 
         // 2. sweep slab rows t = -A .. RW+AR-1 through a ring of horizontal
         //    sums (hu, hv) and vertical pair sums q(t) = h(t) + h(t+1)
@@ -765,7 +775,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         }
         // single-buffered exchange: the neighbours' reads of this iteration
         // must finish before the next iteration's publish overwrites them
+#ifndef HSFLOW_DEV_NOBAR
         if constexpr (wg_nbuf(W, RW) == 1) __syncthreads();
+#endif
     }
 
     asm volatile("; slab parity %0 sweep end" ::"n"(PAR));
