@@ -43,6 +43,10 @@ struct JacobiArgs {
                                // in the product library
     int band_w;                // K2 workgroup kernel: tile-column band width
                                // of the tile order (0 = row-major; launcher)
+#ifdef HSFLOW_DEV_TRACE
+    long trace_base;           // development builds: first trace record of
+                               // this launch (-1: off)
+#endif
 };
 
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,

@@ -35,6 +35,31 @@
 #include "hsflow_internal.h"
 #include "hsflow_device.h"
 
+#ifdef HSFLOW_DEV_TRACE
+#include <atomic>
+// Development builds only: per-workgroup phase timestamps of the K2
+// workgroup kernel (s_memrealtime, 100 MHz) -- entry, operator set-up done,
+// iterations done, stores issued -- plus the hardware ids, written by lane
+// 0..5 of wave 0 with vector buffer stores.  scripts/k2_trace.py reads them.
+namespace hsflow {
+constexpr long kTraceCap = 1L << 18;  // workgroup records
+__device__ unsigned long long g_k2_trace[kTraceCap * 6];
+static std::atomic<long> g_trace_next{0};
+}  // namespace hsflow
+extern "C" __attribute__((visibility("default"))) int hsflow_dev_trace_read(
+    void *host, size_t max_records, size_t *n) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    long cnt = hsflow::g_trace_next.exchange(0);
+    size_t m = (size_t)(cnt < hsflow::kTraceCap ? cnt : hsflow::kTraceCap);
+    if (m > max_records) m = max_records;
+    *n = m;
+    if (m && hipMemcpyFromSymbol(host, HIP_SYMBOL(hsflow::g_k2_trace), m * 48, 0,
+                                 hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return 0;
+}
+#endif
+
 namespace hsflow {
 
 
@@ -397,6 +422,11 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                                             plane_bytes);
 }
 
+template <int W, int KB, int RW, int NW, int SB>
+__device__ __forceinline__ void wg_tile(const JacobiArgs &p,
+                                        float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
+                                        float2 *tpl, int logical);
+
 // 4 waves per SIMD (<= 128 VGPRs): two 8-wave workgroups per CU
 template <int W, int KB, int RW, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiArgs p) {
@@ -418,10 +448,24 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     const int nblk = gridDim.x * gridDim.y;
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
     const int qn = nblk >> 3, rem = nblk & 7, xcd = lin & 7;
-    const int logical = xcd * qn + min(xcd, rem) + (lin >> 3);
-    const int pair = logical / gridDim.x;
-    const int tile = logical - pair * gridDim.x;
-    if (tile >= p.tiles_x * p.tiles_y) return;  // whole workgroup: uniform
+    wg_tile<W, KB, RW, NW, SB>(p, xch, tpl, xcd * qn + min(xcd, rem) + (lin >> 3));
+}
+
+// One tile (logical index: pair-major, then the tile order) of the
+// workgroup kernel: pick the body variant and run it.
+template <int W, int KB, int RW, int NW, int SB>
+__device__ __forceinline__ void wg_tile(const JacobiArgs &p,
+                                        float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
+                                        float2 *tpl, int logical) {
+    constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
+    constexpr int HL = KB * A, HR = KB * AR;
+    constexpr int HLc = HL + (HL & 1), HRc = HR + (HR & 1);
+    constexpr int RX = 128, RY = NW * RW;
+    constexpr int OX = RX - HLc - HRc, OY = RY - HL - HR;
+    const int ntile = p.tiles_x * p.tiles_y;
+    const int pair = logical / ntile;
+    const int tile = logical - pair * ntile;
+    if (pair >= p.batch) return;  // whole workgroup: uniform
     // Tile order inside a pair: row-major, or (band_w > 0) bands of band_w
     // tile columns walked row-major one band after the other, so that a
     // tile's upper neighbour was loaded band_w (not tiles_x) workgroups
@@ -454,7 +498,11 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     // (same tiles, same operator, any blocking depth).
     const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols &&
                           ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows;
+#ifdef HSFLOW_DEV_NOFLAG  // development ablation: no flags read (packed only)
+    const bool g32 = false;
+#else
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
+#endif
     if (g32) {
         if ((cols & 1) == 0)
             wg_body<W, KB, RW, NW, SB, true, true, true>(p, xch, tpl, tx, ty, wv, lane, pbase,
@@ -491,6 +539,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     // sinking the two parity bodies' identical load and store code into the
     // shared path (which costs ~50 spilled VGPRs at 11-row slabs)
     asm volatile("; slab parity %0 begin" ::"n"(PAR));
+#ifdef HSFLOW_DEV_TRACE
+    const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
+#endif
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
     constexpr int HL = KB * A, HR = KB * AR;
     constexpr int HLc = HL + (HL & 1), HRc = HR + (HR & 1);
@@ -602,6 +653,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         }
     }
 
+#ifdef HSFLOW_DEV_TRACE
+    const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
+#endif
     const float inv = p.inv_w2;
     const f2v invv = {inv, inv};
     auto t_row = [&](int y) -> f2v {
@@ -633,7 +687,38 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     // w = 3: Q at even rows, S(y) = h(y-1) + Q(y), S(y+1) = Q(y) + h(y+2).
     // 2 (w = 5) and 1.5 (w = 3) adds per row and field instead of 3 and 2.
     constexpr bool SHARED = W == 3 || W == 5;
-    for (int it = 0; it < n_it; ++it) {
+    // output descriptors and this lane's store offset: the last iteration
+    // stores each row as soon as it is final (the stores drain under the
+    // rest of the sweep instead of holding the workgroup slot after it)
+    const auto uo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_out + pbase), 0,
+                                                         nbytes, 0x00020000);
+    const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
+                                                         nbytes, 0x00020000);
+    const bool st_lane = lane >= HLc / 2 && lane < (HLc + OX) / 2;
+    auto store_row = [&](int r, int vo_e, int vo_o) {
+        const int wr = wv * RW + r;  // workgroup region row (wave-uniform)
+        if (!(wr >= HL && wr < HL + OY && ((rowmask >> r) & 1ull))) return;
+        const int so = (r0 + r) * cols * 4;
+        if constexpr (X2) {
+            __builtin_amdgcn_raw_buffer_store_b64(
+                u2v{__float_as_uint(U[r].x), __float_as_uint(U[r].y)}, uo_rs, vo_e, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(
+                u2v{__float_as_uint(V[r].x), __float_as_uint(V[r].y)}, vo_rs, vo_e, so, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].x), uo_rs, vo_e, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].y), uo_rs, vo_o, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].x), vo_rs, vo_e, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, vo_o, so, 0);
+        }
+    };
+    auto iteration = [&](int it, auto last_c) {
+        constexpr bool LAST = decltype(last_c)::value;
+        int vo_e = 0, vo_o = 0;
+        if constexpr (LAST) {
+            const int c4 = launder(gce * 4);
+            vo_e = (st_lane && ce) ? c4 : kOOB;
+            vo_o = (st_lane && co) ? c4 + 4 : kOOB;
+        }
         const int par = wg_nbuf(W, RW) == 2 ? (it & 1) : 0;
         // 1. horizontal sums of the boundary rows first, published for the
         //    neighbouring slabs: rows 0..AR-1 feed the wave above, rows
@@ -770,43 +855,52 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                 }
                 U[y] = nu;
                 V[y] = nv;
+                if constexpr (LAST) store_row(y, vo_e, vo_o);
             }
             if ((rr % SB) == SB - 1) __builtin_amdgcn_sched_barrier(0);
         }
         // single-buffered exchange: the neighbours' reads of this iteration
         // must finish before the next iteration's publish overwrites them
 #ifndef HSFLOW_DEV_NOBAR
-        if constexpr (wg_nbuf(W, RW) == 1) __syncthreads();
+        if constexpr (!LAST && wg_nbuf(W, RW) == 1) __syncthreads();
 #endif
-    }
+    };
+    int it = 0;
+    for (; it + 1 < n_it; ++it) iteration(it, std::false_type{});
+    if (it < n_it) iteration(it, std::true_type{});
 
     asm volatile("; slab parity %0 sweep end" ::"n"(PAR));
-    // interior tile: workgroup rows [HL, HL + OY), lanes [HLc/2, (HLc + OX)/2)
-    const auto uo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_out + pbase), 0,
-                                                         nbytes, 0x00020000);
-    const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
-                                                         nbytes, 0x00020000);
-    const bool st_lane = lane >= HLc / 2 && lane < (HLc + OX) / 2;
-    const int off0 = launder((r0 * cols + gce) * 4);
+#ifdef HSFLOW_DEV_TRACE
+    const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
+#endif
+    // no iteration ran (iters = 0): the loaded state is the output
+    if (n_it == 0) {
+        const int c4 = launder(gce * 4);
+        const int vo_e = (st_lane && ce) ? c4 : kOOB;
+        const int vo_o = (st_lane && co) ? c4 + 4 : kOOB;
 #pragma unroll
-    for (int r = 0; r < RW; ++r) {
-        const int wr = wv * RW + r;  // workgroup region row (wave-uniform)
-        const bool rin = wr >= HL && wr < HL + OY && ((rowmask >> r) & 1ull);
-        if constexpr (X2) {
-            const int o = (rin && st_lane && ce) ? off0 + r * cols * 4 : kOOB;
-            __builtin_amdgcn_raw_buffer_store_b64(
-                u2v{__float_as_uint(U[r].x), __float_as_uint(U[r].y)}, uo_rs, o, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(
-                u2v{__float_as_uint(V[r].x), __float_as_uint(V[r].y)}, vo_rs, o, 0, 0);
-        } else {
-            const int oe = (rin && st_lane && ce) ? off0 + r * cols * 4 : kOOB;
-            const int oo = (rin && st_lane && co) ? off0 + r * cols * 4 + 4 : kOOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].x), uo_rs, oe, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].y), uo_rs, oo, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].x), vo_rs, oe, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, oo, 0, 0);
-        }
+        for (int r = 0; r < RW; ++r) store_row(r, vo_e, vo_o);
     }
+#ifdef HSFLOW_DEV_TRACE
+    {
+        const uint64_t tr3 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+        const long rec = p.trace_base +
+                         (long)(pbase / ((size_t)p.rows * cols)) * (p.tiles_x * p.tiles_y) +
+                         (long)ty * p.tiles_x + tx;
+        const uint64_t meta = (uint64_t)hwid | ((uint64_t)xcc << 32);
+        const uint64_t tile = (uint64_t)(unsigned)tx | ((uint64_t)(unsigned)ty << 16) |
+                              ((uint64_t)blockIdx.x << 32);
+        const uint64_t val = lane == 0 ? tr0 : lane == 1 ? tr1 : lane == 2 ? tr2
+                           : lane == 3 ? tr3 : lane == 4 ? meta : tile;
+        const bool on = wv == 0 && lane < 6 && p.trace_base >= 0 && rec < kTraceCap;
+        const auto trs = __builtin_amdgcn_make_buffer_rsrc((void *)g_k2_trace, 0,
+                                                           (int)(kTraceCap * 48), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)val, (uint32_t)(val >> 32)}, trs,
+                                              on ? (int)((rec * 6 + lane) * 8) : kOOB, 0, 0);
+    }
+#endif
     asm volatile("; slab parity %0 end" ::"n"(PAR));
 }
 
@@ -967,6 +1061,13 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     static const int band_env = probe_env("HSFLOW_K2_BAND", 0);
     a.band_w = band_env;
     static const unsigned extra_lds = (unsigned)probe_env("HSFLOW_EXTRA_LDS", 0);
+#ifdef HSFLOW_DEV_TRACE
+    {
+        static const bool on = getenv("HSFLOW_DEV_TRACE_ON") != nullptr;
+        const long n = (long)ntiles * a.batch;
+        a.trace_base = on ? g_trace_next.fetch_add(n) : -1;
+    }
+#endif
     hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW, SB>), grd, dim3(NW * 64),
                        extra_lds, s, a);
     return hipGetLastError();
