@@ -537,8 +537,12 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
         stream = [tuple(torch.from_numpy(a).to(dev) for a in
                         hsflow.synth_pair(1000 + j, rows, cols)) for j in range(n)]
     mine = fp.my_pairs(n, rank, world)
+    # N > 1: each rank's share in 2 groups, so group 0's (u, v) travel back
+    # while group 1 is solved (frame_parallel.run_stream_pipelined); one
+    # rank has nothing to overlap and solves its share in one call
+    chunks = 2 if world > 1 else 1
     if solve_batch is None:
-        ws = hsflow.alloc_workspace(rows, cols, max(1, len(mine)), dev)
+        ws = hsflow.alloc_workspace(rows, cols, max(1, -(-len(mine) // chunks)), dev)
 
         def solve_batch(I0, I1):
             return hsflow.flow_device(I0, I1, args.window, iters, args.alpha, workspace=ws)
@@ -546,19 +550,15 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
     out = [None]
 
     def one_pass():
-        pairs = fp.scatter_pairs(stream, n, (rows, cols), torch.float32, dev, rank, world)
-        flows = []
-        if pairs:
-            u, v = solve_batch(torch.stack([p[0] for p in pairs]),
-                               torch.stack([p[1] for p in pairs]))
-            flows = [(u[k], v[k]) for k in range(len(pairs))]
-        out[0] = fp.gather_flows(flows, n, (rows, cols), dev, rank, world)
+        out[0] = fp.run_stream_pipelined(stream, n, (rows, cols), torch.float32, solve_batch,
+                                         dev, rank, world, chunks=chunks)
 
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     steps = max(1, min(args.steps, 3))
     elapsed = timed_region(one_pass, sync, steps, 1, world, dev)
     leg = {"pairs_per_s": round(n * steps / elapsed, 2),
            "ms_per_pass": round(elapsed / steps * 1e3, 3), "pairs": n,
+           "groups_per_rank": chunks,
            "Mpix_iter_per_s": round(n * steps * rows * cols * iters / elapsed / 1e6, 1),
            "transport": ("RCCL point-to-point" if world > 1 and dev.type == "cuda"
                          else ("gloo" if world > 1 else "none (one rank)")),

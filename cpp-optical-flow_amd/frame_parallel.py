@@ -105,6 +105,119 @@ def run_stream(stream: Optional[Sequence[Pair]], n_pairs: int, shape, dtype,
     return gather_flows(flows, n_pairs, shape, device, rank, world)
 
 
+def chunk_split(mine: Sequence[int], chunks: int) -> List[List[int]]:
+    """This rank's pairs cut into at most `chunks` contiguous groups (sizes
+    differ by at most one, larger groups first; no empty groups)."""
+    n = len(mine)
+    k = max(1, min(chunks, n)) if n else 0
+    out, start = [], 0
+    for c in range(k):
+        size = n // k + (1 if c < n % k else 0)
+        out.append(list(mine[start:start + size]))
+        start += size
+    return out
+
+
+def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, dtype,
+                         solve_batch: Callable[[torch.Tensor, torch.Tensor], Pair], device,
+                         rank: int, world: int, chunks: int = 2, gather: bool = True):
+    """run_stream with the transfers overlapped: each rank's share is cut into
+    `chunks` groups; rank 0 posts the scatter of every group at once, a rank
+    solves group c (one batched call) as soon as group c has arrived --
+    group c+1 is still in flight -- and sends group c's (u, v) back while it
+    solves group c+1.  With RCCL every step is stream-ordered: work.wait()
+    makes the compute stream wait on the communicator's stream, so no host
+    blocking until rank 0 collects the result.
+
+    The point-to-point calls are issued in the same order on both ends of
+    every link (all scatter groups, then the gather groups in group order),
+    which is what keeps RCCL's in-order matching free of deadlock: a rank
+    posts its receives for every group before its first result send.
+    Returns rank 0's (u, v) list in stream order (None elsewhere, or when
+    gather=False).  Bit-identical to run_stream: only the schedule changes."""
+    mine = my_pairs(n_pairs, rank, world)
+    if world == 1:
+        out: List[Pair] = []
+        for grp in chunk_split(mine, chunks):
+            I0 = torch.stack([stream[j][0].to(device) for j in grp])
+            I1 = torch.stack([stream[j][1].to(device) for j in grp])
+            u, v = solve_batch(I0, I1)
+            out.extend((u[k], v[k]) for k in range(len(grp)))
+        return out if gather else None
+    groups = {r: chunk_split(my_pairs(n_pairs, r, world), chunks) for r in range(world)}
+    n_groups = max(len(g) for g in groups.values())
+    # 1. scatter: every group of every rank posted up front, group-major
+    recv_groups: List[Tuple[torch.Tensor, torch.Tensor, list]] = []
+    if rank == 0:
+        ops = []
+        for c in range(n_groups):
+            for dst in range(1, world):
+                if c >= len(groups[dst]):
+                    continue
+                for j in groups[dst][c]:
+                    I0, I1 = stream[j]
+                    ops.append(dist.P2POp(dist.isend, I0.to(device).contiguous(), dst))
+                    ops.append(dist.P2POp(dist.isend, I1.to(device).contiguous(), dst))
+        scatter_reqs = dist.batch_isend_irecv(ops) if ops else []
+    else:
+        for grp in groups[rank]:
+            a = torch.empty((len(grp),) + tuple(shape), dtype=dtype, device=device)
+            b = torch.empty((len(grp),) + tuple(shape), dtype=dtype, device=device)
+            ops = []
+            for k in range(len(grp)):
+                ops.append(dist.P2POp(dist.irecv, a[k], 0))
+                ops.append(dist.P2POp(dist.irecv, b[k], 0))
+            recv_groups.append((a, b, dist.batch_isend_irecv(ops)))
+    # 2. per group: solve, then ship the result (rank 0 posts its receives
+    #    of the remote ranks' group c first, so they need not wait behind
+    #    its own solve of group c on the communicator's stream)
+    result: List[Optional[Pair]] = [None] * n_pairs
+    pending = []
+    for c in range(n_groups):
+        if rank == 0 and gather:  # posted before rank 0's own solve c
+            ops = []
+            for src in range(1, world):
+                if c >= len(groups[src]):
+                    continue
+                for j in groups[src][c]:
+                    u = torch.empty(tuple(shape), dtype=torch.float32, device=device)
+                    v = torch.empty(tuple(shape), dtype=torch.float32, device=device)
+                    ops.append(dist.P2POp(dist.irecv, u, src))
+                    ops.append(dist.P2POp(dist.irecv, v, src))
+                    result[j] = (u, v)
+            if ops:
+                pending.append((None, None, dist.batch_isend_irecv(ops)))
+        if c < len(groups[rank]):
+            grp = groups[rank][c]
+            if rank == 0:
+                I0 = torch.stack([stream[j][0].to(device) for j in grp])
+                I1 = torch.stack([stream[j][1].to(device) for j in grp])
+            else:
+                I0, I1, reqs = recv_groups[c]
+                for req in reqs:
+                    req.wait()
+            u, v = solve_batch(I0, I1)
+            if rank == 0:
+                for k, j in enumerate(grp):
+                    result[j] = (u[k], v[k])
+            elif gather:
+                u, v = u.contiguous(), v.contiguous()
+                ops = []
+                for k in range(len(grp)):
+                    ops.append(dist.P2POp(dist.isend, u[k], 0))
+                    ops.append(dist.P2POp(dist.isend, v[k], 0))
+                pending.append((u, v, dist.batch_isend_irecv(ops)))
+    if rank == 0:
+        for req in scatter_reqs:
+            req.wait()
+    for _, _, reqs in pending:
+        for req in reqs:
+            req.wait()
+    if not gather:
+        return None
+    return result if rank == 0 else None
+
+
 def max_over_ranks(seconds: float, device, world: int) -> float:
     """The bench's timing rule: the slowest rank defines the step time."""
     if world == 1:

@@ -140,7 +140,7 @@ def _free_port():
     return p
 
 
-def _c4_worker(rank, world, port, q):
+def _c4_worker(rank, world, port, q, pipelined=False):
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, ROOT, os.path.join(ROOT, "cpp-optical-flow_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -152,16 +152,26 @@ def _c4_worker(rank, world, port, q):
         mine = fp.my_pairs(C4_PAIRS, rank, world)
         ws = hsflow.alloc_workspace(C4_ROWS, C4_COLS, len(mine), "cuda")
         # transport: gloo with host tensors (both ranks share the one GPU);
-        # each rank solves its share in one batched call on cuda:0
-        pairs = fp.scatter_pairs(stream, C4_PAIRS, (C4_ROWS, C4_COLS), torch.float32,
-                                 torch.device("cpu"), rank, world)
-        u, v = hsflow.flow_device(torch.stack([p[0] for p in pairs]).cuda(),
-                                  torch.stack([p[1] for p in pairs]).cuda(), 5, C4_ITERS,
-                                  1.0, workspace=ws)
-        torch.cuda.synchronize()
-        flows = [(u[k].cpu(), v[k].cpu()) for k in range(len(pairs))]
-        out = fp.gather_flows(flows, C4_PAIRS, (C4_ROWS, C4_COLS), torch.device("cpu"),
-                              rank, world)
+        # each rank solves its share (or each group of it) in one batched
+        # call on cuda:0
+        if pipelined:
+            def solve_batch(I0, I1):
+                u, v = hsflow.flow_device(I0.cuda(), I1.cuda(), 5, C4_ITERS, 1.0, workspace=ws)
+                torch.cuda.synchronize()
+                return u.cpu(), v.cpu()
+            out = fp.run_stream_pipelined(stream, C4_PAIRS, (C4_ROWS, C4_COLS), torch.float32,
+                                          solve_batch, torch.device("cpu"), rank, world,
+                                          chunks=2)
+        else:
+            pairs = fp.scatter_pairs(stream, C4_PAIRS, (C4_ROWS, C4_COLS), torch.float32,
+                                     torch.device("cpu"), rank, world)
+            u, v = hsflow.flow_device(torch.stack([p[0] for p in pairs]).cuda(),
+                                      torch.stack([p[1] for p in pairs]).cuda(), 5, C4_ITERS,
+                                      1.0, workspace=ws)
+            torch.cuda.synchronize()
+            flows = [(u[k].cpu(), v[k].cpu()) for k in range(len(pairs))]
+            out = fp.gather_flows(flows, C4_PAIRS, (C4_ROWS, C4_COLS), torch.device("cpu"),
+                                  rank, world)
         q.put(("ok", [_c4_digest(a, b) for a, b in out]) if rank == 0 else ("peer", None))
     except Exception as e:  # pragma: no cover
         q.put(("err", repr(e)))
@@ -169,11 +179,15 @@ def _c4_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_config4_stream_64_pairs_two_ranks_bit_identical(hs):
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_config4_stream_64_pairs_two_ranks_bit_identical(hs, pipelined):
+    """Config 4 over two ranks: the serial schedule (scatter, solve, gather)
+    and bench.py's overlapped one (frame_parallel.run_stream_pipelined, two
+    groups per rank) both return every pair's single-GPU bits."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_c4_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_c4_worker, args=(r, 2, port, q, pipelined)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=200) for _ in procs]

@@ -93,6 +93,72 @@ def test_single_rank_path():
     assert len(out) == N_PAIRS
 
 
+def _solve_batch(I0, I1):
+    us, vs = zip(*[_solve(a, b) for a, b in zip(I0, I1)])
+    return torch.stack(us), torch.stack(vs)
+
+
+def _pipe_worker(rank, world, port, chunks, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [here, os.path.join(root, "oracle"), os.path.join(root, "cpp-optical-flow_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        stream = _stream() if rank == 0 else None
+        out = fp.run_stream_pipelined(stream, N_PAIRS, (ROWS, COLS), torch.float32,
+                                      _solve_batch, torch.device("cpu"), rank, world,
+                                      chunks=chunks)
+        q.put(("ok", [(u.numpy(), v.numpy()) for (u, v) in out]) if rank == 0
+              else ("peer", out))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chunk_split():
+    assert fp.chunk_split([0, 2, 4, 6], 2) == [[0, 2], [4, 6]]
+    assert fp.chunk_split([1, 3, 5], 2) == [[1, 3], [5]]
+    assert fp.chunk_split([1], 3) == [[1]]
+    assert fp.chunk_split([], 2) == []
+    assert sum(fp.chunk_split(list(range(9)), 4), []) == list(range(9))
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 2), (3, 2), (2, 3), (3, 1)])
+def test_pipelined_stream_bit_identical(world, chunks):
+    """The overlapped schedule (scatter of every group posted up front, group
+    c+1 solved while group c's flows travel back) returns every pair's flow
+    in stream order, equal to the per-pair solve, for uneven shares (7 pairs
+    over 2 and 3 ranks) and any group count."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, chunks, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] != "err" for r in res), res
+    assert all(r[1] is None for r in res if r[0] == "peer")
+    flows = [r for r in res if r[0] == "ok"][0][1]
+    assert len(flows) == N_PAIRS
+    for j, (I0, I1) in enumerate(_stream()):
+        u, v = _solve(I0, I1)
+        assert np.array_equal(flows[j][0], u.numpy()) and np.array_equal(flows[j][1], v.numpy())
+
+
+def test_pipelined_single_rank_groups():
+    out = fp.run_stream_pipelined(_stream(), N_PAIRS, (ROWS, COLS), torch.float32,
+                                  _solve_batch, torch.device("cpu"), 0, 1, chunks=3)
+    for j, (I0, I1) in enumerate(_stream()):
+        u, v = _solve(I0, I1)
+        assert np.array_equal(out[j][0].numpy(), u.numpy())
+
+
 # ---- the same protocol with the real HIP solver (2 processes, one GPU) ----
 
 def _gpu_solve(I0, I1):
