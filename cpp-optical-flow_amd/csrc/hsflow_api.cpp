@@ -187,13 +187,14 @@ int max_split() {
 }
 
 SidePool *side_pool(int need) {
-    thread_local SidePool pool;
+    // one pool per device and thread: a thread that alternates devices keeps
+    // each device's streams (re-creating them per switch would leak them)
+    thread_local std::vector<SidePool> pools;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    if (pool.device != dev) {
-        pool = SidePool();
-        pool.device = dev;
-    }
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+    if ((int)pools.size() <= dev) pools.resize(dev + 1);
+    SidePool &pool = pools[dev];
+    pool.device = dev;
     while ((int)pool.streams.size() < need) {
         hipStream_t st;
         if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
