@@ -45,31 +45,9 @@ namespace {
 thread_local std::string g_err;  // errors from calls without a context
 int g_kb_override = 0;
 // Jacobi pass kernel (hsflow_set_jacobi_kernel): 0 = automatic, 2 = K2 tiles,
-// one launch per pass, 4 = dataflow K2 (one launch per solve) wherever it
-// exists (windows 3 and 5 at their default blocking).  All run the K2 tile
-// body (the persistent K2p and the streaming K3 alternatives measured slower
-// and were retired).
+// one launch per pass -- both run K2 (the persistent K2p and the streaming
+// K3 alternatives measured slower and were retired)
 int g_kernel_override = 0;
-#ifdef HSFLOW_DEV_DF
-constexpr bool kDfAuto = true;
-#else
-constexpr bool kDfAuto = false;
-#endif
-
-// compute units of the current device (cached per device id)
-int cur_device_cus() {
-    static int per_dev[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (per_dev[dev] == 0) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                hipSuccess || cus <= 0)
-            return 0;
-        per_dev[dev] = cus;
-    }
-    return per_dev[dev];
-}
 
 int fail(hsflow_ctx *ctx, int code, const char *fmt, ...) {
     char buf[512];
@@ -115,7 +93,6 @@ struct Workspace {
     uint32_t *gpack;
     float *gx, *gy, *gt, *u2, *v2;
     uint32_t *flags;
-    int *dfctl;  // dataflow K2 control block (queue heads, done counters)
     size_t bytes;
 };
 
@@ -135,7 +112,6 @@ Workspace carve(void *base, int rows, int cols, int batch) {
     w.u2 = (float *)take(n * 4);
     w.v2 = (float *)take(n * 4);
     w.flags = (uint32_t *)take((size_t)batch * 4);
-    w.dfctl = (int *)take(hsflow::df_ctl_bytes(rows, cols, batch));
     w.bytes = off;
     return w;
 }
@@ -164,16 +140,6 @@ int pick_kb(int window, bool need_f32) {
     int kb = hsflow::default_kb(window);
     while (kb > 1 && !hsflow::kb_supported(window, kb, need_f32)) kb /= 2;
     return kb;
-}
-
-// One dataflow launch for the whole solve instead of a launch per pass?
-// Automatic: batches of whole multiples of 8 pairs (one XCD per pair, every
-// XCD equally loaded) on the full 256-CU MI355X.
-bool use_df(int window, int iters, int batch, bool maybe_f32) {
-    if (iters == 0 || g_kernel_override == 2) return false;
-    if (!hsflow::df_supported(window, pick_kb(window, maybe_f32))) return false;
-    if (g_kernel_override == 4) return true;
-    return kDfAuto && batch % 8 == 0 && cur_device_cus() == 256;
 }
 
 // Per-thread, per-device side streams for splitting a batch: each sub-batch
@@ -258,7 +224,7 @@ int jacobi_impl(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int 
     int rc0 = check_jacobi_args(ctx, rows, cols, batch, window, iters, u, v, workspace,
                                 ws_bytes);
     if (rc0) return rc0;
-    const int split = use_df(window, iters, batch, maybe_f32) ? 1 : std::min(batch, max_split());
+    const int split = std::min(batch, max_split());
     if (split <= 1 || iters == 0)
         return jacobi_one(ctx, rows, cols, batch, window, iters, alpha, warm, maybe_f32, u,
                           v, workspace, ws_bytes, s);
@@ -329,29 +295,6 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
             src_v = v;
         }
     }
-    if (w.dfctl != nullptr && use_df(window, iters, batch, maybe_f32)) {
-        const int cus = cur_device_cus();
-        if (cus <= 0) return fail(ctx, HSFLOW_ERR_HIP, "device CU count unavailable");
-        HIP_TRY(ctx, hipMemsetAsync(w.dfctl, 0, hsflow::df_ctl_bytes(rows, cols, batch), s));
-        hsflow::DfArgs d{};
-        d.a = a;
-        d.u0 = src_u;
-        d.v0 = src_v;
-        d.ua = u;
-        d.va = v;
-        d.ub = w.u2;
-        d.vb = w.v2;
-        d.passes = passes;
-        d.kb = kb;
-        d.iters = iters;
-        d.queue = w.dfctl;
-        d.err = w.dfctl + 8 * hsflow::kDfQueueStride;
-        d.cuctr = w.dfctl + 8 * hsflow::kDfQueueStride + 64;
-        d.done = d.cuctr + 8 * 256;
-        hipError_t e = hsflow::launch_jacobi_df(d, window, kb, cus, s);
-        if (e != hipSuccess) return hip_fail(ctx, e, "jacobi dataflow launch");
-        return HSFLOW_OK;
-    }
     int done = 0;
     for (int pass = 0; pass < passes; ++pass) {
         a.iters = std::min(kb, iters - done);
@@ -408,7 +351,6 @@ int jacobi_sub(hsflow_ctx *ctx, int rows, int cols, int nb, int first, int batch
     sub.u2 = w.u2 + off;
     sub.v2 = w.v2 + off;
     sub.flags = w.flags + first;
-    sub.dfctl = nullptr;  // a sub-batch of a split runs per-pass launches
     return run_passes(ctx, rows, cols, nb, window, iters, alpha, warm, maybe_f32, u, v, sub,
                       s);
 }
@@ -734,7 +676,7 @@ int hsflow_set_iters_per_launch(int k) {
 }
 
 int hsflow_set_jacobi_kernel(int k) {
-    if (k != 0 && k != 2 && k != 4) return HSFLOW_ERR_ARG;
+    if (k != 0 && k != 2) return HSFLOW_ERR_ARG;
     g_kernel_override = k;
     return HSFLOW_OK;
 }

@@ -49,39 +49,10 @@ struct JacobiArgs {
 #endif
 };
 
-// Dataflow K2: ONE launch runs every pass of a solve.  Workgroups stay
-// resident and pull (pass, pair, tile) items from a per-XCD queue; an item
-// starts once the 3 x 3 neighbourhood of its tile has finished the previous
-// pass (per-tile done counters), so there is no per-pass launch boundary and
-// no per-workgroup dispatch gap.  Pair j is solved on XCD j % 8 only, so every
-// hand-off stays inside one XCD's L2 (coherent for the XCD's CUs; loads of
-// the handed-off planes bypass L1).
-struct DfArgs {
-    JacobiArgs a;              // shared fields (gradients, sizes, alpha, ...)
-    const float *u0, *v0;      // pass-0 input (null: u = v = 0)
-    float *ua, *va;            // caller's planes: the last pass lands here
-    float *ub, *vb;            // workspace planes (ping-pong partner)
-    int passes, kb, iters;
-    int *queue;                // 8 heads, kDfQueueStride ints apart
-    int *done;                 // [batch][tiles]: passes finished per tile
-    int *err;                  // set if a dependency wait timed out
-    int *cuctr;                // [8][256] workgroups started per CU
-};
-constexpr int kDfQueueStride = 32;  // ints (128 B): one head per cache line
-// control block bytes: 8 queue heads + the done counters + the error word
-inline size_t df_ctl_bytes(int rows, int cols, int batch) {
-    // tiles of every dataflow geometry (output tiles >= 64 x 64) fit this
-    const size_t tiles = (size_t)((rows + 31) / 32) * (size_t)((cols + 63) / 64);
-    return (size_t)(8 * kDfQueueStride + 64 + 8 * 256) * 4 + tiles * (size_t)batch * 4;
-}
-
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
                             int cols, int batch, uint32_t *gpack, float *gx, float *gy,
                             float *gt, uint32_t *flags, hipStream_t s);
 hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s);
-// dataflow K2 for (W, KB) where supported: false = use per-pass launches
-bool df_supported(int W, int KB);
-hipError_t launch_jacobi_df(DfArgs d, int W, int KB, int cus, hipStream_t s);
 // config 5 pyramid (hsflow_pyramid.hip); dtype as HSFLOW_U8/F32/F16
 hipError_t launch_pyrdown(const void *src, int dtype, int rows, int cols, int batch,
                           float *dst, const uint32_t *flags, hipStream_t s);

@@ -375,28 +375,6 @@ __global__ __launch_bounds__(256) void hs_jacobi_kernel(const JacobiArgs p) {
 //    origins are even for every KB), so every KB gives identical bits.
 
 
-// Dataflow K2 (hs_jacobi_df_kernel below): a workgroup's loop state, kept in
-// LDS rather than SGPRs (the tile body needs all 102 SGPRs, so anything live
-// across it would spill), and shared with the tile body, which fetches the
-// next work item during its loads and publishes the previous tile after its
-// first barrier.
-struct DfLds {
-    float *ou[2], *ov[2];  // output planes: [0] workspace, [1] caller's
-    const float *u0, *v0;  // pass-0 input
-    int *done, *err, *q;
-    int item, ok;          // next work item; dependency check result
-    int prev, prev_val;    // previous tile (pair * tiles + tile, -1: none)
-};
-__shared__ DfLds g_dfl;    // allocated only by the kernels that use it
-
-template <class T>
-__device__ __forceinline__ T *uniform_ptr(T *p) {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (T *)(((uint64_t)hi << 32) | lo);
-}
-
 // workgroup-kernel geometry per window: slab rows per wave (deeper register
 // rings for wider windows) and double-buffered slab exchange while two
 // workgroups' W-1 boundary rows fit in LDS
@@ -418,7 +396,7 @@ constexpr int wg_rows_tl(int W) {
 }
 
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32, bool ROWE,
-          int PAR, bool DF>
+          int PAR>
 __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                                           float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
                                           float2 *tpl, int tx, int ty, int wv, int lane,
@@ -428,7 +406,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
 // order of the vertical sums follows image-row parity, see wg_body_p): a
 // whole body per parity, so no register state lives across the two.
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32,
-          bool ROWE = true, bool DF = false>
+          bool ROWE = true>
 __device__ __forceinline__ void wg_body(const JacobiArgs &p,
                                         float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64], float2 *tpl,
                                         int tx, int ty, int wv, int lane, size_t pbase,
@@ -437,14 +415,14 @@ __device__ __forceinline__ void wg_body(const JacobiArgs &p,
     constexpr int OY = NW * RW - KB * A - KB * AR;
     const int r0 = ty * OY - KB * A + wv * RW;
     if ((W == 3 || W == 5) && (r0 & 1))
-        wg_body_p<W, KB, RW, NW, SB, EDGE, X2, G32, ROWE, 1, DF>(p, xch, tpl, tx, ty, wv, lane,
-                                                                pbase, plane_bytes);
+        wg_body_p<W, KB, RW, NW, SB, EDGE, X2, G32, ROWE, 1>(p, xch, tpl, tx, ty, wv, lane, pbase,
+                                                            plane_bytes);
     else
-        wg_body_p<W, KB, RW, NW, SB, EDGE, X2, G32, ROWE, 0, DF>(p, xch, tpl, tx, ty, wv, lane,
-                                                                pbase, plane_bytes);
+        wg_body_p<W, KB, RW, NW, SB, EDGE, X2, G32, ROWE, 0>(p, xch, tpl, tx, ty, wv, lane, pbase,
+                                                            plane_bytes);
 }
 
-template <int W, int KB, int RW, int NW, int SB, bool DF = false>
+template <int W, int KB, int RW, int NW, int SB>
 __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
                                         float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
                                         float2 *tpl, int logical);
@@ -473,157 +451,9 @@ __global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiAr
     wg_tile<W, KB, RW, NW, SB>(p, xch, tpl, xcd * qn + min(xcd, rem) + (lin >> 3));
 }
 
-// ------------------------------------------------------------- K2 dataflow
-// hs_jacobi_df_kernel: every pass of a solve in ONE launch (DfArgs in
-// hsflow_internal.h).  Each workgroup loops: take the next (pass, pair, tile)
-// item of its XCD's queue, wait until the tile's 3 x 3 neighbourhood has
-// finished the previous pass (which also means those workgroups have read
-// this tile's region of the plane this pass overwrites), run the K2 tile
-// body.  The body fetches the following item during its loads and publishes
-// the previous tile's done counter after its first barrier, when that
-// tile's stores are complete.  Items are dealt pass-major, so a tile's
-// dependencies were dequeued about one pass earlier and the wait is one
-// load.  Pair j lives on XCD j % 8: hand-offs stay inside one L2.
-constexpr long kDfSpinMax = 1L << 22;  // ~2 s of polling: report, do not hang
-
-
-template <int W, int KB, int RW, int NW, int SB>
-__global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_df_kernel(const DfArgs d) {
-    constexpr int NB = W - 1;
-    __shared__ float2 xch[wg_nbuf(W, RW)][NW][NB][2][64];
-    __shared__ float2 tpl[wg_tlds(W, RW) ? NW * RW * 64 : 1];
-    auto geometry = [](int tiles_x, int tiles_y, int batch, int passes, int &xcc, int &ntile,
-                       int &per_pass, int &total) {
-        xcc = (int)(__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u);
-        ntile = tiles_x * tiles_y;
-        per_pass = ((batch - xcc + 7) / 8) * ntile;  // pairs xcc, xcc + 8, ...
-        total = passes * per_pass;
-    };
-    {
-        int xcc, ntile, per_pass, total;
-        geometry(d.a.tiles_x, d.a.tiles_y, d.a.batch, d.passes, xcc, ntile, per_pass, total);
-        if (threadIdx.x == 0) {
-            g_dfl.ou[0] = d.ub;
-            g_dfl.ov[0] = d.vb;
-            g_dfl.ou[1] = d.ua;
-            g_dfl.ov[1] = d.va;
-            g_dfl.u0 = d.u0;
-            g_dfl.v0 = d.v0;
-            g_dfl.done = d.done;
-            g_dfl.err = d.err;
-            g_dfl.q = d.queue + xcc * kDfQueueStride;
-#ifdef HSFLOW_DEV_DF_STAGGER
-            // the second workgroup of each CU starts later, so the two
-            // co-resident workgroups are out of phase (one loads while the
-            // other iterates) for the whole solve
-            {
-                const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
-                const int key = (int)(((hw >> 13) & 7u) * 32 + ((hw >> 12) & 1u) * 16 +
-                                      ((hw >> 8) & 15u));
-                if (atomicAdd(d.cuctr + xcc * 256 + key, 1) & 1)
-                    for (int k = 0; k < HSFLOW_DEV_DF_STAGGER; ++k)
-                        __builtin_amdgcn_s_sleep(127);
-            }
-#endif
-            g_dfl.item = total > 0 ? atomicAdd(g_dfl.q, 1) : 0;
-            g_dfl.prev = -1;
-        }
-    }
-    __syncthreads();
-    for (;;) {
-        // the arguments are re-read from the kernarg segment per item (a
-        // laundered pointer: scalar loads the compiler cannot hoist), so
-        // none of them is held in an SGPR across the previous tile's body
-#ifdef __HIP_DEVICE_COMPILE__
-        typedef const DfArgs __attribute__((address_space(4))) KArgs;
-        KArgs *K = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(K));
-        KArgs &D = *K;
-#else
-        const DfArgs &D = d;
-#endif
-        int xcc, ntile, per_pass, total;
-        geometry(D.a.tiles_x, D.a.tiles_y, D.a.batch, D.passes, xcc, ntile, per_pass, total);
-        const int item = __builtin_amdgcn_readfirstlane(g_dfl.item);
-        if (item >= total) break;
-        const int pass = item / per_pass;
-        const int rem = item - pass * per_pass;
-        const int lp = rem / ntile;
-        const int tile = rem - lp * ntile;
-        const int pair = xcc + 8 * lp;
-        const int tiles_x = D.a.tiles_x, tiles_y = D.a.tiles_y;
-        if (pass > 0) {
-            // wave 0: lanes 0..8 read the 3 x 3 neighbourhood's counters
-            const int l = threadIdx.x & 63;
-            const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-            const int nx = tx + l % 3 - 1, ny = ty + l / 3 - 1;
-            const bool need = l < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < tiles_y;
-            auto ready = [&]() {
-                const int *f = g_dfl.done + (size_t)pair * ntile + (need ? ny * tiles_x + nx : 0);
-                const bool ok = !need || __hip_atomic_load(f, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT) >= pass;
-                return __builtin_amdgcn_ballot_w64(!ok) == 0;
-            };
-            if (threadIdx.x < 64) {
-                const bool ok = ready();
-                if (threadIdx.x == 0) g_dfl.ok = ok ? 1 : 0;
-            }
-            __syncthreads();  // the other waves load only after the check
-            if (g_dfl.ok == 0) {
-                // Not ready (rare: items are dealt a pass apart).  Publish
-                // this workgroup's previous tile before waiting, so that no
-                // two workgroups can wait on each other's unpublished tile.
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (threadIdx.x == 0 && g_dfl.prev >= 0) {
-                    __hip_atomic_store(g_dfl.done + g_dfl.prev, g_dfl.prev_val,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    g_dfl.prev = -1;
-                }
-                __syncthreads();  // every wave sees prev = -1 before the body
-                if (threadIdx.x < 64) {
-                    for (long spin = 0; !ready(); ++spin) {
-                        if (spin >= kDfSpinMax) {
-                            if (threadIdx.x == 0) atomicOr(g_dfl.err, 1);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        JacobiArgs t = D.a;
-        t.iters = min(D.kb, D.iters - pass * D.kb);
-#ifdef HSFLOW_DEV_TRACE
-        if (t.trace_base >= 0) t.trace_base += (long)pass * D.a.batch * ntile;
-#endif
-        // pass k writes the caller's planes iff (passes - 1 - k) is even
-        const int ko = ((D.passes - 1 - pass) & 1) == 0 ? 1 : 0;
-        // (LDS reads are per lane: readfirstlane keeps the planes in SGPRs)
-        t.u_in = uniform_ptr(pass == 0 ? g_dfl.u0 : g_dfl.ou[ko ^ 1]);
-        t.v_in = uniform_ptr(pass == 0 ? g_dfl.v0 : g_dfl.ov[ko ^ 1]);
-        t.u_out = uniform_ptr(g_dfl.ou[ko]);
-        t.v_out = uniform_ptr(g_dfl.ov[ko]);
-        wg_tile<W, KB, RW, NW, SB, true>(t, xch, tpl, pair * ntile + tile);
-        __syncthreads();  // g_dfl.item written, prev published; LDS free
-        if (threadIdx.x == 0) {
-            g_dfl.prev = pair * ntile + tile;
-            g_dfl.prev_val = pass + 1;
-        }
-        // (the next check's or body's first barrier orders these writes)
-    }
-    // the last tile: every wave's stores complete, then its counter
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0 && g_dfl.prev >= 0)
-        __hip_atomic_store(g_dfl.done + g_dfl.prev, g_dfl.prev_val, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // One tile (logical index: pair-major, then the tile order) of the
 // workgroup kernel: pick the body variant and run it.
-template <int W, int KB, int RW, int NW, int SB, bool DF>
+template <int W, int KB, int RW, int NW, int SB>
 __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
                                         float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
                                         float2 *tpl, int logical) {
@@ -675,32 +505,32 @@ __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
 #endif
     if (g32) {
         if ((cols & 1) == 0)
-            wg_body<W, KB, RW, NW, SB, true, true, true, true, DF>(p, xch, tpl, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, true, true, true>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                          plane_bytes);
         else
-            wg_body<W, KB, RW, NW, SB, true, false, true, true, DF>(p, xch, tpl, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, true, false, true>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                           plane_bytes);
         return;
     }
     if ((cols & 1) == 0) {
         if (interior)
-            wg_body<W, KB, RW, NW, SB, false, true, false, true, DF>(p, xch, tpl, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, false, true, false>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                            plane_bytes);
         else if (W <= 7 && ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows)
             // left/right border tiles: every region row inside the image
-            wg_body<W, KB, RW, NW, SB, true, true, false, false, DF>(p, xch, tpl, tx, ty, wv,
+            wg_body<W, KB, RW, NW, SB, true, true, false, false>(p, xch, tpl, tx, ty, wv,
                                                                  lane, pbase, plane_bytes);
         else
-            wg_body<W, KB, RW, NW, SB, true, true, false, true, DF>(p, xch, tpl, tx, ty, wv, lane, pbase,
+            wg_body<W, KB, RW, NW, SB, true, true, false>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                           plane_bytes);
     } else {
-        wg_body<W, KB, RW, NW, SB, true, false, false, true, DF>(p, xch, tpl, tx, ty, wv, lane, pbase,
+        wg_body<W, KB, RW, NW, SB, true, false, false>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                        plane_bytes);
     }
 }
 
 template <int W, int KB, int RW, int NW, int SB, bool EDGE, bool X2, bool G32, bool ROWE,
-          int PAR, bool DF>
+          int PAR>
 __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                                           float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
                                           float2 *tpl, int tx, int ty, int wv, int lane,
@@ -753,15 +583,6 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     const auto gt_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gt + pbase), 0,
                                                          G32 ? nbytes : 0, 0x00020000);
 
-    // Dataflow K2: the workgroup's next work item is fetched now, during
-    // this tile's loads (published to LDS after the first barrier), and the
-    // u, v planes another workgroup of this XCD wrote are read past this
-    // CU's L1 (sc1: served by the XCD's L2, where the writer's stores are).
-    constexpr int LAUX = DF ? 16 : 0;  // cache policy of the u, v loads
-    int nxt = 0;
-    if constexpr (DF) {
-        if (threadIdx.x == 0) nxt = atomicAdd(g_dfl.q, 1);
-    }
     // (even, odd) column pairs as 2-wide vectors: the identical per-column
     // arithmetic issues as packed FP32 (v_pk_add/mul/fma_f32), one
     // instruction for both columns (on gfx950 a wave64 VALU op costs ~4 SIMD
@@ -784,8 +605,8 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
             if constexpr (X2) {
                 const int o = (!EDGE || (((rowmask >> r) & 1ull) && ce))
                                   ? off0 + r * cols * 4 : kOOB;
-                const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, LAUX);
-                const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, LAUX);
+                const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, 0);
+                const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, 0);
                 U[r] = f2v{__uint_as_float(a.x), __uint_as_float(a.y)};
                 V[r] = f2v{__uint_as_float(b.x), __uint_as_float(b.y)};
                 if constexpr (G32) {
@@ -804,10 +625,10 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                 const bool rin = (rowmask >> r) & 1ull;
                 const int oe = (rin && ce) ? off0 + r * cols * 4 : kOOB;
                 const int oo = (rin && co) ? off0 + r * cols * 4 + 4 : kOOB;
-                U[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oe, 0, LAUX));
-                U[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, LAUX));
-                V[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, LAUX));
-                V[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, LAUX));
+                U[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oe, 0, 0));
+                U[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(u_rs, oo, 0, 0));
+                V[r].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oe, 0, 0));
+                V[r].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_rs, oo, 0, 0));
                 if constexpr (G32) {
                     ixe = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gx_rs, oe, 0, 0));
                     ixo = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gx_rs, oo, 0, 0));
@@ -919,19 +740,6 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
 #ifndef HSFLOW_DEV_NOBAR  // development ablation: timing without the barriers
         __syncthreads();
 #endif
-        if constexpr (DF) {
-            // Every wave has consumed all its loads of this tile (operator
-            // set-up), so -- vector memory operations retiring in order --
-            // the stores of its previous tile are complete in the XCD's L2:
-            // publish that tile's done counter, and the next item.
-            if (it == 0 && threadIdx.x == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                g_dfl.item = nxt;
-                if (g_dfl.prev >= 0)
-                    __hip_atomic_store(g_dfl.done + g_dfl.prev, g_dfl.prev_val,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
 
         // 2. sweep slab rows t = -A .. RW+AR-1 through a ring of horizontal
         //    sums (hu, hv) and vertical pair sums q(t) = h(t) + h(t+1)
@@ -943,11 +751,11 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         // unconditional, from a clamped slab (no branches, no zero fill).
         const int wa = wv > 0 ? wv - 1 : 0, wb = wv < NW - 1 ? wv + 1 : NW - 1;
         f2v hu[W], hv[W], qu[W], qv[W], mu, mv;
-#ifdef HSFLOW_DEV_TPF
-        // T plane in LDS: read one output row ahead so the LDS latency of
-        // row y+1's operator hides under row y's update
-        f2v tnext = t_row(0);
-#endif
+        // T plane in LDS: interior tiles read it one output row ahead, so
+        // the LDS latency of row y+1's operator hides under row y's update
+        // (+0.7 % at 1080p x 8 and 4K x 2, same box, bit-identical)
+        f2v tnext = f2v{0.f, 0.f};
+        if constexpr (TL && !EDGE) tnext = t_row(0);
 #pragma unroll
         for (int rr = 0; rr < RW + NB; ++rr) {
             const int t = rr - A;
@@ -1047,17 +855,14 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                         nu = f2v{0.f, 0.f};
                         nv = f2v{0.f, 0.f};
                     }
+                } else if constexpr (TL) {
+                    const f2v tcur = tnext;
+                    if (y + 1 < RW) tnext = t_row(y + 1);
+                    // keep the read of row y+1 here: only LDS reads may not
+                    // be moved across (VALU, SALU, VMEM and DS writes may)
+                    __builtin_amdgcn_sched_barrier(0x67E);
+                    op_update(su, sv, invv, X[y], Y[y], tcur, nu, nv);
                 } else {
-#ifdef HSFLOW_DEV_TPF
-                    if constexpr (TL) {
-                        const f2v tcur = tnext;
-                        if (y + 1 < RW) tnext = t_row(y + 1);
-                        // keep the read of row y+1 here: only LDS reads may
-                        // not be moved across (VALU, SALU, VMEM, DS writes may)
-                        __builtin_amdgcn_sched_barrier(0x67E);
-                        op_update(su, sv, invv, X[y], Y[y], tcur, nu, nv);
-                    } else
-#endif
                     op_update(su, sv, invv, X[y], Y[y], t_row(y), nu, nv);
                 }
                 U[y] = nu;
@@ -1351,44 +1156,6 @@ static hipError_t launch_jacobi_w(JacobiArgs a, int KB, hipStream_t s) {
         break;
     default: break;
     }
-    return hipErrorInvalidValue;
-}
-
-// Dataflow K2 (one launch per solve) for the default blocking of windows 3
-// and 5 (the tall T-in-LDS slabs at w = 5, the all-register ones at w = 3);
-// any batch (pairs are dealt to XCDs j % 8).
-bool df_supported(int W, int KB) {
-    if (k2_variant() == 0) return false;
-    return (W == 5 && KB == 6) || (W == 3 && KB == 8);
-}
-
-hipError_t launch_jacobi_df(DfArgs d, int W, int KB, int cus, hipStream_t s) {
-    if (!df_supported(W, KB)) return hipErrorInvalidValue;
-    auto go = [&](auto kern, int RW) {
-        const int HL = KB * (W - W / 2 - 1), HR = KB * (W / 2);
-        const int ox = 128 - (HL + (HL & 1)) - (HR + (HR & 1));
-        const int oy = 8 * RW - KB * (W - 1);
-        d.a.tiles_x = (d.a.cols + ox - 1) / ox;
-        d.a.tiles_y = (d.a.rows + oy - 1) / oy;
-        d.a.band_w = 0;
-#ifdef HSFLOW_DEV_TRACE
-        {
-            static const bool on = getenv("HSFLOW_DEV_TRACE_ON") != nullptr;
-            const long n = (long)d.a.tiles_x * d.a.tiles_y * d.a.batch * d.passes;
-            d.a.trace_base = on ? g_trace_next.fetch_add(n) : -1;
-        }
-#endif
-        // two resident workgroups per CU (LDS and 128 VGPRs); a larger grid
-        // would only add workgroups that find their queue empty
-        hipLaunchKernelGGL(kern, dim3((unsigned)(2 * cus)), dim3(512), 0, s, d);
-        return hipGetLastError();
-    };
-#if !defined(HSFLOW_DEV_W) || HSFLOW_DEV_W == 5
-    if (W == 5) return go(hs_jacobi_df_kernel<5, 6, wg_rows_tl(5), 8, 16>, wg_rows_tl(5));
-#endif
-#if !defined(HSFLOW_DEV_W) || HSFLOW_DEV_W == 3
-    if (W == 3) return go(hs_jacobi_df_kernel<3, 8, wg_rows(3), 8, 16>, wg_rows(3));
-#endif
     return hipErrorInvalidValue;
 }
 
