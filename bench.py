@@ -519,6 +519,19 @@ def e2e_leg(wl_name, args, dev, n_batches=12):
 
 
 # --------------------------------------------------------------- stream
+def _transport(world, dev):
+    """What moved the stream leg's pairs: RCCL only for CUDA tensors under
+    the nccl backend (the gloo rehearsal on one GPU stages through the host
+    and says so)."""
+    if world == 1:
+        return "none (one rank)"
+    import torch.distributed as dist
+    backend = dist.get_backend()
+    if backend == "nccl" and dev.type == "cuda":
+        return "RCCL point-to-point"
+    return f"{backend} ({dev.type} tensors)"
+
+
 def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
     """BASELINE config 4: a stream of n_pairs synthetic frame pairs held by
     rank 0, scattered one-per-rank round-robin (point-to-point over RCCL;
@@ -560,8 +573,7 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
            "ms_per_pass": round(elapsed / steps * 1e3, 3), "pairs": n,
            "groups_per_rank": chunks,
            "Mpix_iter_per_s": round(n * steps * rows * cols * iters / elapsed / 1e6, 1),
-           "transport": ("RCCL point-to-point" if world > 1 and dev.type == "cuda"
-                         else ("gloo" if world > 1 else "none (one rank)")),
+           "transport": _transport(world, dev),
            "scaling": "strong"}
     if rank == 0:
         res = out[0]

@@ -81,7 +81,7 @@ def test_bench_n2_timing_and_stream_leg_over_gloo():
     assert res[0][1] == res[1][1] and res[0][1] >= 0.15
     leg0, leg1 = res[0][2], res[1][2]
     assert isinstance(leg0, dict), leg0
-    assert leg0["gathered"] == N_PAIRS and leg0["finite"] and leg0["transport"] == "gloo"
+    assert leg0["gathered"] == N_PAIRS and leg0["finite"] and leg0["transport"] == "gloo (cpu tensors)"
     assert leg0["pairs_per_s"] == leg1["pairs_per_s"] > 0  # max-over-ranks time
 
 
