@@ -111,6 +111,9 @@ def parse(argv=None):
                          "ONE pair split into row bands with a halo exchange")
     ap.add_argument("--chunk", type=int, default=12,
                     help="bands mode: iterations between halo exchanges")
+    ap.add_argument("--overlap", action="store_true",
+                    help="bands mode: hide each exchange behind the next chunk's interior "
+                         "(row_bands.solve_overlapped; bit-identical)")
     ap.add_argument("--pairs", type=int, default=64, help="stream leg: pairs in the stream")
     return ap.parse_args(argv)
 
@@ -775,8 +778,11 @@ def bands_mode(args, world, rank, dev):
     comm = rb.DistComm() if world > 1 else rb.LocalComm()
     res = [None]
 
+    overlap = bool(args.overlap) and rb.overlap_ok(p)
+    solve = rb.solve_overlapped if overlap else rb.solve
+
     def one():
-        states = rb.solve([I0], [I1], p, iters, ops, comm, [rank])
+        states = solve([I0], [I1], p, iters, ops, comm, [rank])
         res[0] = rb.gather_owned(states, p, comm)
 
     elapsed = timed_region(one, lambda: torch.cuda.synchronize(dev), args.steps, args.warmup,
@@ -795,6 +801,8 @@ def bands_mode(args, world, rank, dev):
             "dtype": "f32", "data": f"synthetic {in_dtype} frame pair",
             "config": {"workload": f"{cols}x{rows}, {levels} levels, {iters} it/level",
                        "window": args.window, "chunk": args.chunk, "halo_rows": p.halo,
+                       "exchange": "overlapped with interior iterations" if overlap
+                       else "after every chunk",
                        "parallelism": f"row bands x{world}"},
             "parity": parity}), flush=True)
     if world > 1:

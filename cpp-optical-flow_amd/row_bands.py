@@ -144,11 +144,45 @@ class DeviceOps:
     def set_zero(self, x):
         x.zero_()
 
+    # overlapped schedule (solve_overlapped): the interior runs on a side
+    # stream, the edge strips and the exchange on the caller's stream
+    def clone(self, x):
+        return x.clone()
+
+    def cat_rows(self, a, b):
+        return self.torch.cat([a, b], 0)
+
+    def copy_rows(self, dst, src):
+        dst.copy_(src)
+
+    def _main(self):
+        return self.torch.cuda.current_stream(self.device) if self.stream is None else self.stream
+
+    def fork(self):
+        if not hasattr(self, "_side"):
+            self._side = self.torch.cuda.Stream(device=self.device)
+        self._side.wait_stream(self._main())
+
+    def jacobi_side(self, ws, u, v, n: int):
+        r, c = u.shape
+        self.hs.jacobi_device(r, c, 1, self.window, n, self.alpha, u, v, ws,
+                              warm_start=True, stream=self._side)
+
+    def join(self):
+        self._main().wait_stream(self._side)
+
 
 # -------------------------------------------------------------------- comm
 class LocalComm:
     """N virtual ranks in one process (tests, one-GPU rehearsal): the halo
     exchange is a copy between the ranks' planes."""
+
+    def start(self, states: Sequence["RankState"], level: int):
+        self.exchange(states, level)
+        return None
+
+    def wait(self, handle):
+        pass
 
     def exchange(self, states: Sequence["RankState"], level: int):
         p = states[0].plan
@@ -166,6 +200,15 @@ class DistComm:
     "nccl" backend; numpy / CPU tensors under "gloo")."""
 
     def exchange(self, states: Sequence["RankState"], level: int):
+        self.wait(self.start(states, level))
+
+    def wait(self, handle):
+        for req in handle or ():
+            req.wait()
+
+    def start(self, states: Sequence["RankState"], level: int):
+        """Post the halo exchange; returns the requests (wait() completes
+        them: a stream wait under RCCL, a host wait under gloo)."""
         import torch
         import torch.distributed as dist
         (s,) = states
@@ -175,16 +218,16 @@ class DistComm:
 
         def t(x):
             return torch.from_numpy(x) if isinstance(x, np.ndarray) else x
+        # send copies: the overlapped schedule rewrites the owned rows (its
+        # next interior solve) while a send may still be reading them
         for f in (s.u[level], s.v[level]):
             if r > 0:
-                ops.append(dist.P2POp(dist.isend, t(f[band.a:band.a + H]), r - 1))
+                ops.append(dist.P2POp(dist.isend, t(f[band.a:band.a + H]).clone(), r - 1))
                 ops.append(dist.P2POp(dist.irecv, t(f[band.a - H:band.a]), r - 1))
             if r < p.world - 1:
-                ops.append(dist.P2POp(dist.isend, t(f[band.b - H:band.b]), r + 1))
+                ops.append(dist.P2POp(dist.isend, t(f[band.b - H:band.b]).clone(), r + 1))
                 ops.append(dist.P2POp(dist.irecv, t(f[band.b:band.b + H]), r + 1))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        return dist.batch_isend_irecv(ops) if ops else []
 
 
 # ------------------------------------------------------------------ solver
@@ -231,6 +274,131 @@ def solve(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
         for s in states:
             if l + 1 < p.levels:
                 s.u[l + 1] = s.v[l + 1] = None     # coarse level no longer needed
+    return states
+
+
+def _clone(ops, x):
+    if hasattr(ops, "clone"):
+        return ops.clone(x)
+    return x if isinstance(x, tuple) else x.copy()  # numpy (oracle-backed ops)
+
+
+def _cat(ops, a, b):
+    return ops.cat_rows(a, b) if hasattr(ops, "cat_rows") else np.concatenate([a, b], 0)
+
+
+def _copy(ops, dst, src):
+    if hasattr(ops, "copy_rows"):
+        ops.copy_rows(dst, src)
+    else:
+        dst[...] = src
+
+
+def overlap_ok(p: Plan) -> bool:
+    """The overlapped schedule needs every band to hold two halos of rows
+    (its edge strips' valid rows and the interior's must tile the band)."""
+    return p.world > 1 and all(bd.b - bd.a >= 2 * p.halo for lv in p.bands for bd in lv)
+
+
+def solve_overlapped(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
+    """solve() with each chunk's halo exchange hidden behind the next
+    chunk's interior iterations.  Per rank and chunk, with H = p.halo and the
+    owned rows [a, b):
+      * the interior [a, b) is solved in place as its own plane: its edges at
+        a and b are artificial, so after the chunk its rows [a + H, b - H) are
+        exact -- and it needs nothing from the neighbours, so it runs (on a
+        side stream on the GPU) while the previous chunk's exchange is in
+        flight;
+      * the edge strips [a - H, a + 2H) and [b - 2H, b + H) -- the received
+        halo rows plus a snapshot of the owned rows taken before the interior
+        overwrites them -- are solved once the exchange has landed, on the
+        caller's stream, concurrently with the interior; their middle thirds
+        are the exact rows [a, a + H) and [b - H, b), written back (after
+        the interior has finished) and sent to the neighbours as copies
+        (posted, not waited for: the next interior solve may rewrite the
+        rows while a send is still reading).
+    Critical path per chunk: max(interior, exchange + strip) instead of
+    band + exchange.  Every sub-plane starts on an even image row (H and the
+    band starts are even), so every owned row is BIT-IDENTICAL to solve()
+    and to the undivided solve.  Gradients of the three sub-planes are
+    computed once per level (their artificial edges differ from the band's)."""
+    if not overlap_ok(p):
+        raise ValueError("overlapped schedule needs world > 1 and bands of >= 2 halos")
+    H = p.halo
+    states = [RankState(p, r, ops) for r, ops in zip(ranks, ops_list)]
+    for s, I0, I1 in zip(states, I0s, I1s):
+        s.P0, s.P1 = s.ops.levels(I0, I1, p.levels)
+
+    for l in range(p.levels - 1, -1, -1):
+        R, C = p.sizes[l]
+        g = []
+        for s in states:
+            bd = p.bands[l][s.rank]
+            s.u[l], s.v[l] = s.ops.zeros(R, C), s.ops.zeros(R, C)
+            if l < p.levels - 1:
+                c0 = bd.e0 // 2
+                c1 = min(p.sizes[l + 1][0], (bd.e1 + 1) // 2)
+                s.ops.upflow(s.u[l + 1][c0:c1], s.v[l + 1][c0:c1],
+                             s.u[l][bd.e0:bd.e1], s.v[l][bd.e0:bd.e1])
+            top = bd.a > 0
+            bot = bd.b < R
+            # DeviceOps computes gradients into one reused workspace: each
+            # sub-plane keeps its own copy (which also holds its solve's
+            # ping-pong planes, so interior and strips can run concurrently)
+            gi = _clone(s.ops, s.ops.gradients(s.P0[l][bd.a:bd.b], s.P1[l][bd.a:bd.b]))
+            gt = _clone(s.ops, s.ops.gradients(s.P0[l][bd.a - H:bd.a + 2 * H],
+                                               s.P1[l][bd.a - H:bd.a + 2 * H])) if top else None
+            gb = _clone(s.ops, s.ops.gradients(s.P0[l][bd.b - 2 * H:bd.b + H],
+                                               s.P1[l][bd.b - 2 * H:bd.b + H])) if bot else None
+            g.append((gi, gt, gb, top, bot))
+        pending = None
+        done = 0
+        while done < iters:
+            n = min(p.chunk, iters - done)
+            snaps = []
+            for s, (gi, gt, gb, top, bot) in zip(states, g):
+                bd = p.bands[l][s.rank]
+                u, v = s.u[l], s.v[l]
+                # the owned rows the strips need, before the interior moves on
+                snaps.append((_clone(s.ops, u[bd.a:bd.a + 2 * H]) if top else None,
+                              _clone(s.ops, v[bd.a:bd.a + 2 * H]) if top else None,
+                              _clone(s.ops, u[bd.b - 2 * H:bd.b]) if bot else None,
+                              _clone(s.ops, v[bd.b - 2 * H:bd.b]) if bot else None))
+                if hasattr(s.ops, "fork"):  # interior on the side stream
+                    s.ops.fork()
+                    s.ops.jacobi_side(gi, u[bd.a:bd.b], v[bd.a:bd.b], n)
+                else:
+                    s.ops.jacobi(gi, u[bd.a:bd.b], v[bd.a:bd.b], n)
+            comm.wait(pending)                                     # chunk - 1's halos
+            strips = []
+            for s, (gi, gt, gb, top, bot), (tu, tv, bu, bv) in zip(states, g, snaps):
+                bd = p.bands[l][s.rank]
+                u, v = s.u[l], s.v[l]
+                st = sb = None
+                if top:
+                    st = (_cat(s.ops, u[bd.a - H:bd.a], tu), _cat(s.ops, v[bd.a - H:bd.a], tv))
+                    s.ops.jacobi(gt, st[0], st[1], n)
+                if bot:
+                    sb = (_cat(s.ops, bu, u[bd.b:bd.b + H]), _cat(s.ops, bv, v[bd.b:bd.b + H]))
+                    s.ops.jacobi(gb, sb[0], sb[1], n)
+                strips.append((st, sb))
+            for s, (st, sb) in zip(states, strips):
+                bd = p.bands[l][s.rank]
+                u, v = s.u[l], s.v[l]
+                if hasattr(s.ops, "join"):
+                    s.ops.join()
+                if st is not None:
+                    _copy(s.ops, u[bd.a:bd.a + H], st[0][H:2 * H])
+                    _copy(s.ops, v[bd.a:bd.a + H], st[1][H:2 * H])
+                if sb is not None:
+                    _copy(s.ops, u[bd.b - H:bd.b], sb[0][H:2 * H])
+                    _copy(s.ops, v[bd.b - H:bd.b], sb[1][H:2 * H])
+            pending = comm.start(states, l)
+            done += n
+        comm.wait(pending)
+        for s in states:
+            if l + 1 < p.levels:
+                s.u[l + 1] = s.v[l + 1] = None
     return states
 
 

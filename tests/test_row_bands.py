@@ -99,6 +99,32 @@ def test_local_bands_equal_undivided_oracle(world, levels, chunk, window):
     assert np.array_equal(u, uo) and np.array_equal(v, vo)
 
 
+@pytest.mark.parametrize("world,levels,chunk,window,iters", [(2, 2, 3, 5, 7), (3, 1, 2, 5, 9),
+                                                             (4, 2, 2, 3, 5), (2, 1, 3, 5, 3)])
+def test_local_overlapped_bands_equal_undivided_oracle(world, levels, chunk, window, iters):
+    """The overlapped schedule (interior solved while the halos travel,
+    edge strips solved from the received halos and a snapshot) gives the
+    undivided solve's bits, like the plain schedule."""
+    I0, I1 = _pair(101, 53)
+    p = rb.plan(101, 53, levels, world, window, chunk)
+    assert rb.overlap_ok(p)
+    comm = rb.LocalComm()
+    ops = [OracleOps(window, 1.0) for _ in range(world)]
+    states = rb.solve_overlapped([I0] * world, [I1] * world, p, iters, ops, comm,
+                                 list(range(world)))
+    u, v = rb.gather_owned(states, p, comm)
+    uo, vo = oracle.flow_pyramid(I0, I1, levels, window, iters, 1.0)
+    assert np.array_equal(u, uo) and np.array_equal(v, vo)
+
+
+def test_overlap_needs_two_halos_per_band():
+    p = rb.plan(60, 30, 1, 3, 5, 6)   # bands of 20 rows, halo 12
+    assert not rb.overlap_ok(p)
+    with pytest.raises(ValueError):
+        rb.solve_overlapped([None] * 3, [None] * 3, p, 4, [None] * 3, rb.LocalComm(), [0, 1, 2])
+    assert not rb.overlap_ok(rb.plan(60, 30, 1, 1, 5, 2))   # nothing to overlap on one rank
+
+
 def test_local_bands_non_integral_frames():
     I0, I1 = _pair(66, 41)
     I0 = I0 * np.float32(0.7) + np.float32(0.2)
@@ -120,10 +146,10 @@ def _free_port():
     return port
 
 
-ROWS, COLS, LEVELS, ITERS, CHUNK = 72, 45, 2, 8, 3
+ROWS, COLS, LEVELS, ITERS, CHUNK = 104, 45, 2, 8, 3
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
@@ -134,7 +160,8 @@ def _worker(rank, world, port, q):
         I0, I1 = synth_pair(1000, ROWS, COLS)
         p = rb.plan(ROWS, COLS, LEVELS, world, 5, CHUNK)
         comm = rb.DistComm()
-        states = rb.solve([I0], [I1], p, ITERS, [OracleOps(5, 1.0)], comm, [rank])
+        solve = rb.solve_overlapped if overlap else rb.solve
+        states = solve([I0], [I1], p, ITERS, [OracleOps(5, 1.0)], comm, [rank])
         u, v = rb.gather_owned(states, p, comm)
         q.put(("ok", rank, None if u is None else (u.copy(), v.copy())))
     except Exception as e:  # pragma: no cover
@@ -143,12 +170,16 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_bands_equal_undivided_oracle(world):
+@pytest.mark.parametrize("world,overlap", [(2, False), (3, False), (2, True), (3, True)])
+def test_gloo_bands_equal_undivided_oracle(world, overlap):
+    """Plain and overlapped schedules over torch.distributed point-to-point
+    (the code RCCL runs): the posted-then-waited exchange, send copies and
+    all, gives the undivided solve's bits."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, overlap))
+             for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=180) for _ in range(world)]
@@ -170,7 +201,8 @@ def hs():
     return hsflow
 
 
-def _bands_on_one_gpu(hs, I0, I1, levels, window, iters, world, chunk, dtype=None):
+def _bands_on_one_gpu(hs, I0, I1, levels, window, iters, world, chunk, dtype=None,
+                      overlap=False):
     t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
     if dtype is not None:
         t0, t1 = t0.to(dtype), t1.to(dtype)
@@ -178,7 +210,8 @@ def _bands_on_one_gpu(hs, I0, I1, levels, window, iters, world, chunk, dtype=Non
     p = rb.plan(rows, cols, levels, world, window, chunk)
     ops = [rb.DeviceOps(window, 1.0, t0.device) for _ in range(world)]
     comm = rb.LocalComm()
-    states = rb.solve([t0] * world, [t1] * world, p, iters, ops, comm, list(range(world)))
+    solve = rb.solve_overlapped if overlap else rb.solve
+    states = solve([t0] * world, [t1] * world, p, iters, ops, comm, list(range(world)))
     u, v = rb.gather_owned(states, p, comm)
     ref = hs.flow_pyramid_device(t0, t1, levels, window, iters, 1.0)
     torch.cuda.synchronize()
@@ -191,6 +224,25 @@ def _bands_on_one_gpu(hs, I0, I1, levels, window, iters, world, chunk, dtype=Non
 def test_device_bands_bit_identical_to_single_gpu(hs, world, levels, chunk, window):
     I0, I1 = hs.synth_pair(1000, 400, 522)
     (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, levels, window, 40, world, chunk)
+    assert torch.equal(u, ur) and torch.equal(v, vr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,levels,chunk,window", [(2, 3, 6, 5), (3, 2, 8, 3)])
+def test_device_overlapped_bands_bit_identical_to_single_gpu(hs, world, levels, chunk, window):
+    """The overlapped schedule on the GPU: interiors on each rank's side
+    stream, strips on the caller's stream, in-process exchange."""
+    I0, I1 = hs.synth_pair(1000, 400, 522)
+    (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, levels, window, 40, world, chunk,
+                                         overlap=True)
+    assert torch.equal(u, ur) and torch.equal(v, vr)
+
+
+@pytest.mark.gpu
+def test_device_overlapped_bands_8k_fp16_eight_ranks(hs):
+    I0, I1 = hs.synth_pair(1000, 4320, 7680)
+    (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, 3, 5, 30, 8, 12, torch.float16,
+                                         overlap=True)
     assert torch.equal(u, ur) and torch.equal(v, vr)
 
 
