@@ -133,11 +133,13 @@ bool device_dtype_ok(int dtype) {
     return dtype == HSFLOW_U8 || dtype == HSFLOW_F32 || dtype == HSFLOW_F16;
 }
 
-int pick_kb(int window, bool need_f32) {
+// `batch`: every pair in flight at once (the whole batch, also when it is
+// split over side streams); 0 = shape unknown (no fill adjustment)
+int pick_kb(int window, bool need_f32, int rows = 0, int cols = 0, int batch = 0) {
     if (window > 9) return 1;
     if (g_kb_override > 0 && hsflow::kb_supported(window, g_kb_override, need_f32))
         return g_kb_override;
-    int kb = hsflow::default_kb(window);
+    int kb = hsflow::fill_kb(window, hsflow::default_kb(window), rows, cols, batch);
     while (kb > 1 && !hsflow::kb_supported(window, kb, need_f32)) kb /= 2;
     return kb;
 }
@@ -255,7 +257,7 @@ int jacobi_impl(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int 
 // that may start at any pair of a larger workspace).
 int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int iters,
                float alpha, bool warm, bool maybe_f32, float *u, float *v,
-               const Workspace &w, hipStream_t s) {
+               const Workspace &w, hipStream_t s, int fill_batch) {
     const size_t n = (size_t)rows * cols * batch;
     if (iters == 0) {
         // hornSchunck.cpp:49-50: the loop does not run, u = v = 0
@@ -265,7 +267,7 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         }
         return HSFLOW_OK;
     }
-    const int kb = pick_kb(window, maybe_f32);
+    const int kb = pick_kb(window, maybe_f32, rows, cols, fill_batch);
     const int passes = (iters + kb - 1) / kb;
     JacobiArgs a{};
     a.rows = rows;
@@ -334,14 +336,13 @@ int jacobi_one(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
                                ws_bytes);
     if (rc) return rc;
     return run_passes(ctx, rows, cols, batch, window, iters, alpha, warm, maybe_f32, u, v,
-                      carve(workspace, rows, cols, batch), s);
+                      carve(workspace, rows, cols, batch), s, batch);
 }
 
 // pairs [first, first + nb) of a `batch`-pair workspace w
 int jacobi_sub(hsflow_ctx *ctx, int rows, int cols, int nb, int first, int batch,
                int window, int iters, float alpha, bool warm, bool maybe_f32, float *u,
                float *v, const Workspace &w, hipStream_t s) {
-    (void)batch;
     const size_t off = (size_t)first * rows * cols;
     Workspace sub = w;
     sub.gpack = w.gpack + off;
@@ -351,8 +352,9 @@ int jacobi_sub(hsflow_ctx *ctx, int rows, int cols, int nb, int first, int batch
     sub.u2 = w.u2 + off;
     sub.v2 = w.v2 + off;
     sub.flags = w.flags + first;
+    // the split's halves run concurrently: the depth is chosen for the batch
     return run_passes(ctx, rows, cols, nb, window, iters, alpha, warm, maybe_f32, u, v, sub,
-                      s);
+                      s, batch);
 }
 
 int gradients_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
@@ -688,11 +690,9 @@ int hsflow_set_max_streams(int n) {
 }
 
 int hsflow_iters_per_launch(int rows, int cols, int batch, int window) {
-    (void)rows;
-    (void)cols;
-    (void)batch;
     if (window < 1 || window > HSFLOW_MAX_WINDOW) return HSFLOW_ERR_ARG;
-    return pick_kb(window, true);
+    if (!sizes_ok(rows, cols, batch)) return HSFLOW_ERR_ARG;
+    return pick_kb(window, true, rows, cols, batch);
 }
 
 int hsflow_gradients_device(const void *I0, const void *I1, int dtype_in, int rows,

@@ -62,6 +62,8 @@ hipError_t launch_bgr2gray(const uint8_t *bgr, int rows, int cols, int batch,
 hipError_t launch_upflow(const float *uc, const float *vc, int rc, int cc, float *u,
                          float *v, int rows, int cols, int batch, hipStream_t s);
 int default_kb(int W);
+// default_kb adjusted for launches that do not fill one round of slots
+int fill_kb(int W, int kb, int rows, int cols, int batch);
 bool kb_supported(int W, int KB, bool need_f32);
 
 }  // namespace hsflow

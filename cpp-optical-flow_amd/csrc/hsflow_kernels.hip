@@ -1061,6 +1061,28 @@ static long wg_tiles(const JacobiArgs &a, int W, int KB, int RW) {
     return (long)((a.cols + ox - 1) / ox) * ((a.rows + oy - 1) / oy) * a.batch;
 }
 
+// Blocking depth for a launch that does not fill the chip.  KB = 6 is the
+// measured optimum at w = 5 when a launch has several rounds of workgroups;
+// when one round does not even fill the 2 x CUs slots (a single 1080p pair:
+// 380 workgroups), a pass costs one workgroup lifetime whatever the tile
+// count, so fewer, longer passes win: KB = 8 (its 460 workgroups still fit
+// one round) -- 1080p pair 0.957 -> 0.833 ms, 720p 0.586 -> 0.519 ms, the
+// KITTI 375 x 1242 pair at 100 it 0.209 -> 0.187 ms; a 4K pair (1258
+// workgroups) keeps KB 6 (4.08 vs 4.37 ms).  `batch` counts every pair in
+// flight (a batch split over side streams runs its halves concurrently).
+int fill_kb(int W, int kb, int rows, int cols, int batch) {
+    if (W != 5 || kb != 6 || !uses_wg_kernel(W) || rows <= 0 || cols <= 0 || batch <= 0)
+        return kb;
+    JacobiArgs a{};
+    a.rows = rows;
+    a.cols = cols;
+    a.batch = batch;
+    const long slots = 2L * device_cus();
+    if (wg_tiles(a, 5, 6, wg_rows_tl(5)) >= slots) return kb;
+    const long t8 = std::max(wg_tiles(a, 5, 8, wg_rows_tl(5)), wg_tiles(a, 5, 8, wg_rows(5)));
+    return t8 <= slots ? 8 : kb;
+}
+
 template <int W, int KB, int RW, int NW, int SB>
 static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     constexpr int HL = KB * (W - W / 2 - 1), HR = KB * (W / 2);

@@ -43,7 +43,12 @@ def test_workspace_bytes():
 
 
 def test_iters_per_launch_policy():
-    assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 6  # measured default
+    # measured defaults: w 5 runs 6 iterations per pass when a
+    # launch has rounds of workgroups, 8 when one round does not fill the chip
+    assert hsflow.iters_per_launch(1080, 1920, 8, 5) == 6
+    assert hsflow.iters_per_launch(2160, 3840, 1, 5) == 6
+    assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 8
+    assert hsflow.iters_per_launch(375, 1242, 1, 5) == 8
     assert hsflow.iters_per_launch(1080, 1920, 1, 3) == 8
     assert hsflow.iters_per_launch(1080, 1920, 1, 12) == 1
     with pytest.raises(hsflow.HsflowError):
@@ -51,6 +56,8 @@ def test_iters_per_launch_policy():
     hsflow.set_iters_per_launch(2)
     assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 2
     hsflow.set_iters_per_launch(0)
+    with pytest.raises(Exception):
+        hsflow._check(hsflow.lib().hsflow_iters_per_launch(0, 1920, 1, 5))
 
 
 def test_jacobi_kernel_selector():
