@@ -756,9 +756,12 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         f2v hu[W], hv[W], qu[W], qv[W], mu, mv;
         // T plane in LDS: interior tiles read it one output row ahead, so
         // the LDS latency of row y+1's operator hides under row y's update
-        // (+0.7 % at 1080p x 8 and 4K x 2, same box, bit-identical)
+        // (w = 5: +0.7 % at 1080p x 8 and 4K x 2, same box, bit-identical;
+        // the tall w = 6 and w = 3 slabs have no VGPR left for it: they
+        // spill 8 and 84 B per lane with it)
+        constexpr bool TPF = TL && !EDGE && W == 5;
         f2v tnext = f2v{0.f, 0.f};
-        if constexpr (TL && !EDGE) tnext = t_row(0);
+        if constexpr (TPF) tnext = t_row(0);
 #pragma unroll
         for (int rr = 0; rr < RW + NB; ++rr) {
             const int t = rr - A;
@@ -858,7 +861,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                         nu = f2v{0.f, 0.f};
                         nv = f2v{0.f, 0.f};
                     }
-                } else if constexpr (TL) {
+                } else if constexpr (TPF) {
                     const f2v tcur = tnext;
                     if (y + 1 < RW) tnext = t_row(y + 1);
                     // keep the read of row y+1 here: only LDS reads may not
