@@ -539,6 +539,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     // sinking the two parity bodies' identical load and store code into the
     // shared path (which costs ~50 spilled VGPRs at 11-row slabs)
     asm volatile("; slab parity %0 begin" ::"n"(PAR));
+#ifdef HSFLOW_DEV_PRIO_SETUP  // development: raised wave priority for loads + set-up
+    __builtin_amdgcn_s_setprio(2);
+#endif
 #ifdef HSFLOW_DEV_TRACE
     const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -655,6 +658,12 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
 
 #ifdef HSFLOW_DEV_TRACE
     const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef HSFLOW_DEV_PRIO_SETUP
+    __builtin_amdgcn_s_setprio(0);
+#endif
+#ifdef HSFLOW_DEV_PRIO_ITER  // development: iterating waves above loading ones
+    __builtin_amdgcn_s_setprio(HSFLOW_DEV_PRIO_ITER);
 #endif
     const float inv = p.inv_w2;
     const f2v invv = {inv, inv};
@@ -885,6 +894,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     };
     int it = 0;
     for (; it + 1 < n_it; ++it) iteration(it, std::false_type{});
+#ifdef HSFLOW_DEV_PRIO_LAST  // development: raised wave priority for the storing sweep
+    __builtin_amdgcn_s_setprio(2);
+#endif
     if (it < n_it) iteration(it, std::true_type{});
 
     asm volatile("; slab parity %0 sweep end" ::"n"(PAR));
