@@ -565,6 +565,16 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         rowmask |= (uint64_t)((unsigned)(r0 + r) < (unsigned)p.rows) << r;
 
     constexpr int kOOB = 0x7FFFFFF0;
+#ifdef HSFLOW_DEV_LAUX_UV  // development: cache policy of the u, v slab loads
+    constexpr int LAUX_UV = HSFLOW_DEV_LAUX_UV;
+#else
+    constexpr int LAUX_UV = 0;
+#endif
+#ifdef HSFLOW_DEV_LAUX_G  // development: cache policy of the packed-gradient loads
+    constexpr int LAUX_G = HSFLOW_DEV_LAUX_G;
+#else
+    constexpr int LAUX_G = 0;
+#endif
     const int ablate = kProbeBuild ? p.ablate : 0;  // compiled out of the product
 #ifdef HSFLOW_DEV_NOMEM  // development ablation: loads and stores out of range
     const int nbytes = 0;
@@ -608,8 +618,8 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
             if constexpr (X2) {
                 const int o = (!EDGE || (((rowmask >> r) & 1ull) && ce))
                                   ? off0 + r * cols * 4 : kOOB;
-                const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, 0);
-                const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, 0);
+                const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, LAUX_UV);
+                const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, LAUX_UV);
                 U[r] = f2v{__uint_as_float(a.x), __uint_as_float(a.y)};
                 V[r] = f2v{__uint_as_float(b.x), __uint_as_float(b.y)};
                 if constexpr (G32) {
@@ -620,7 +630,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                     iye = __uint_as_float(gy2.x); iyo = __uint_as_float(gy2.y);
                     ite = __uint_as_float(gt2.x); ito = __uint_as_float(gt2.y);
                 } else {
-                    const u2v g = __builtin_amdgcn_raw_buffer_load_b64(gp_rs, o, 0, 0);
+                    const u2v g = __builtin_amdgcn_raw_buffer_load_b64(gp_rs, o, 0, LAUX_G);
                     unpack_grad(g.x, ixe, iye, ite);
                     unpack_grad(g.y, ixo, iyo, ito);
                 }
