@@ -385,7 +385,11 @@ constexpr bool wg_double_buffer(int W) { return W <= 5; }
 // (32 KB exchange + 48 KB T plane each)
 // Any slab taller than the all-register height wg_rows(W) keeps T in LDS.
 // (w = 3 keeps the double-buffered exchange: 2 boundary rows, 32 KB + 44 KB.)
+#ifdef HSFLOW_DEV_TL_ALWAYS  // development: T plane in LDS at any slab height (w = 5)
+constexpr bool wg_tlds(int W, int RW) { return W == 5 || RW > wg_rows(W); }
+#else
 constexpr bool wg_tlds(int W, int RW) { return RW > wg_rows(W); }
+#endif
 constexpr int wg_nbuf(int W, int RW) {
     return (wg_double_buffer(W) && !(W >= 4 && wg_tlds(W, RW))) ? 2 : 1;
 }
@@ -428,8 +432,13 @@ __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
                                         float2 *tpl, int logical);
 
 // 4 waves per SIMD (<= 128 VGPRs): two 8-wave workgroups per CU
+#ifdef HSFLOW_DEV_WAVES  // development: other occupancy targets
+constexpr int kK2Waves = HSFLOW_DEV_WAVES;
+#else
+constexpr int kK2Waves = 4;
+#endif
 template <int W, int KB, int RW, int NW, int SB>
-__global__ __launch_bounds__(NW * 64, 4) void hs_jacobi_wg_kernel(const JacobiArgs p) {
+__global__ __launch_bounds__(NW * 64, kK2Waves) void hs_jacobi_wg_kernel(const JacobiArgs p) {
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
     constexpr int HL = KB * A, HR = KB * AR;  // temporal halo, rows
     // column halo rounded up to even: region origins stay even for every KB,
@@ -1217,7 +1226,11 @@ hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s) {
     if (W != HSFLOW_DEV_W) return hipErrorInvalidValue;
 #ifdef HSFLOW_DEV_KB
     if (KB != HSFLOW_DEV_KB) return hipErrorInvalidValue;
+#ifdef HSFLOW_DEV_NW  // development: other workgroup geometries
+    return launch_jacobi_wg<HSFLOW_DEV_W, HSFLOW_DEV_KB, HSFLOW_DEV_RW, HSFLOW_DEV_NW, 16>(a, s);
+#else
     return launch_jacobi_wgv<HSFLOW_DEV_W, HSFLOW_DEV_KB>(a, s);
+#endif
 #else
     return launch_jacobi_w<HSFLOW_DEV_W>(a, KB, s);
 #endif
