@@ -12,33 +12,47 @@ torch.distributed over RCCL) solves its own pairs: weak scaling, no
 data-path collective (the timing barrier and max-over-ranks reduction are
 the only collectives in the headline leg).
 
-Rank 0 prints ONE JSON line.  Besides the driver fields it carries
+`--gpus N` is authoritative: without a launcher (no WORLD_SIZE in the
+environment) and N > 1, bench.py starts N rank processes itself
+(torch.distributed.run, 127.0.0.1) and exits with their status; under a
+launcher whose WORLD_SIZE differs from N it refuses to run (status 2).
+
+Rank 0 prints ONE JSON line.  Every timed output is checked: before the
+timed steps the output planes are filled with NaN, so a pass only if the
+timed replays themselves computed (u, v); a parity miss anywhere exits 3.
   parity        pair 0 of the TIMED solve (seed 1000) against the float64
                 oracle's golden checksums (tests/golden/bench_golden.*,
                 made by tests/golden/make_bench_golden.py): max|du|/max|u| on
-                a strided sample and the whole-plane sums.  A mismatch exits
-                non-zero; so does a probe build of the library or any
-                HSFLOW_* diagnostic variable in the environment.
-  roofline      dominant kernel (K2, hs_jacobi_wg_kernel) measured live with
-                events on its launch stream; achieved = SURVEY §8(d)'s 28 B
-                per pixel-iteration x the pixel-iterations of one launch /
-                launch time (> peak is possible: temporal blocking does KB
-                iterations per HBM pass); hbm_frac = PMC bytes per launch
-                (committed profile of this command, profiles/pmc_*.json) /
-                launch time / 8 TB/s; valu_frac = the launch's VALU
-                instructions per SIMD x the measured cycles per instruction
-                of a SIMD running 4 waves (K2's occupancy; ubench) / launch
-                cycles; step_hbm_frac = the PMC bytes of the timed solve
-                (2 side streams) / ms_per_step / 8 TB/s, the HBM rate the
-                timed region sustains (DESIGN.md "Roofline")
-  secondary     the default run also times BASELINE configs[2] (4K x 500 it)
-                with its own roofline and parity check
+                a strided sample and the whole-plane sums
+  parity_all    one verdict per BASELINE config: configs[0] (KITTI crop,
+                host API), [1] (1080p x 300, batched and single pair), [2]
+                (4K x 500, batched and single pair), [3] (the stream of 64
+                pairs: pair 0 vs the golden, pairs 0..7 bit for bit against
+                the resident solve of the same seeds), [4] (8K fp16, 3 levels
+                x 1000 it)
+  roofline      dominant kernel (K2, the Jacobi pass) measured live with
+                events on its launch stream.  achieved = the algorithmic
+                bytes of one temporally blocked pass (read u, v and the
+                packed gradients, write u, v: 20 B per pixel; the first pass
+                reads no u, v) / launch time, frac = achieved / 8 TB/s
+                (a physical fraction, <= 1); traffic / hbm_frac = PMC bytes
+                per launch (committed profile of this command,
+                profiles/pmc_r03.json) / launch time / 8 TB/s;
+                naive_equiv_frac = SURVEY §8(d)'s 28 B per pixel-iteration x
+                the iterations one launch performs / launch time / 8 TB/s
+                (the rate a one-iteration-per-launch kernel would need;
+                exceeds 1 by design, DESIGN.md "Roofline")
+  secondary     BASELINE configs[2] (4K x 2 pairs x 500 it)
+  config5       BASELINE configs[4] (8K fp16, 3-level pyramid, 1000 it/level)
+  single_pair   configs[1] and configs[2] as stated: ONE pair per solve
+                (the reference's call pattern, main.cpp:97-98)
+  window3       north_star's windowSize 3 on the 1080p batch
   pairs_per_s_resident / pairs_per_s_e2e
                 pairs/s with inputs in HBM, and end to end as BASELINE.md
                 defines it: pinned host u8 frames -> H2D -> K1 + K2 -> D2H
                 of (u, v) f32, copies overlapped with solves on other streams
   stream        BASELINE config 4: 64 pairs held by rank 0, scattered over
-                RCCL (point-to-point), solved, (u, v) gathered back
+                RCCL (point-to-point), solved, (u, v) gathered back, checked
   cpu_baseline  the float64 CPU port (oracle/, mirrors hornSchunck.cpp pass
                 by pass) on a bounded sample, 1 thread, rank 0 only
 """
@@ -47,6 +61,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -63,14 +79,13 @@ WORKLOADS = {
 }
 HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 COPY_PEAK_GBPS = 6290.0    # MI355X_MICROARCH.md: float4 copy, measured (79 % of spec)
-VALU_CPI_4W = 3.35         # shader cycles per wave64 VALU instruction of a SIMD
-                           # running 4 waves of independent work, K2's mix of
-                           # v_pk_*_f32 (3.42), DPP adds (3.23) and v_add (3.46):
-                           # scripts/ubench/valu_tput.hip, profiles/r02_valu_tput.txt
-SIMDS = 1024               # 256 CUs x 4
+PASS_BYTES_PER_PX = 20     # one blocked pass: read u, v (8) + packed gradients (4),
+                           # write u, v (8); DESIGN.md "Roofline"
+NAIVE_BYTES_PER_PX_ITER = 28  # f32 u, v, Ix, Iy, It in, u', v' out
 PARITY_TOL = 1e-4          # north_star: 1e-4 relative (norm form)
 GOLDEN_JSON = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 GOLDEN_NPZ = os.path.join(ROOT, "tests", "golden", "bench_golden.npz")
+PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r03.json")
 # HSFLOW_* variables the bench itself reads (rehearsal of the N > 1 logic
 # with several ranks on one GPU); every other HSFLOW_* name is refused
 BENCH_ENV = {"HSFLOW_BENCH_BACKEND", "HSFLOW_BENCH_DEVICE"}
@@ -78,7 +93,8 @@ BENCH_ENV = {"HSFLOW_BENCH_BACKEND", "HSFLOW_BENCH_DEVICE"}
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs = ranks; without a launcher bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p")
@@ -102,6 +118,10 @@ def parse(argv=None):
                     help="skip the configs[2] (4K) block of the default run")
     ap.add_argument("--no-w3", action="store_true",
                     help="skip the window-3 block of the default run (SURVEY §8d)")
+    ap.add_argument("--no-8k", action="store_true",
+                    help="skip the configs[4] (8K pyramid) block of the default run")
+    ap.add_argument("--no-single", action="store_true",
+                    help="skip the single-pair blocks of the default run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pairs/s leg")
     ap.add_argument("--no-stream", action="store_true", help="skip the config-4 stream leg")
     ap.add_argument("--mode", choices=["resident", "stream", "bands"], default="resident",
@@ -115,6 +135,9 @@ def parse(argv=None):
                     help="bands mode: hide each exchange behind the next chunk's interior "
                          "(row_bands.solve_overlapped; bit-identical)")
     ap.add_argument("--pairs", type=int, default=64, help="stream leg: pairs in the stream")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, check they see each other (gloo all-reduce), "
+                         "print n_gpus and exit: the launcher plumbing alone, no GPU work")
     return ap.parse_args(argv)
 
 
@@ -125,6 +148,56 @@ def refuse_diagnostics(environ=None):
     them outright so a stray variable can never produce a number)."""
     environ = os.environ if environ is None else environ
     return sorted(k for k in environ if k.startswith("HSFLOW_") and k not in BENCH_ENV)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def world_from_env(gpus, environ=None):
+    """(action, world): ("launch", N) when N > 1 ranks must be started here
+    (no launcher), ("run", world) under a launcher that agrees with --gpus or
+    for one GPU, ("refuse", world) when WORLD_SIZE contradicts --gpus."""
+    environ = os.environ if environ is None else environ
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        return ("launch", gpus) if gpus > 1 else ("run", 1)
+    world = int(ws)
+    return ("run", world) if world == gpus else ("refuse", world)
+
+
+def launch_ranks(n):
+    """One process per GPU, started the way the driver starts them
+    (torch.distributed.run, one node, 127.0.0.1).  A child process, not an
+    exec: nothing in this process has touched the GPU.  Rank 0's stdout is
+    this process's stdout (the one JSON line)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def launch_check(world, rank):
+    """--launch-check: every rank joins a gloo group and all-reduces a one;
+    rank 0 prints what it saw.  No GPU work (CPU-testable)."""
+    import torch
+    import torch.distributed as dist
+    seen = 1
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": seen,
+                          "launcher": "torch.distributed.run" if world > 1 else "none"}),
+              flush=True)
+    return 0 if seen == world else 4
 
 
 # --------------------------------------------------------------- parity
@@ -192,24 +265,97 @@ def timed_region(step, sync, steps, warmup, world, device):
     return elapsed
 
 
-def pmc_for(workload, kb, batch):
-    """Committed PMC summary (profiles/pmc_<workload>.json) if it was
-    collected for this blocking depth and batch."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if not os.path.exists(path):
+def pmc_key(wl_name, window, batch):
+    return f"{wl_name}_w{window}_b{batch}"
+
+
+def pmc_for(wl_name, window, batch, kb, kernel):
+    """Committed PMC summary of this roofline launch (profiles/pmc_r03.json,
+    written by scripts/pmc_r03.py from separate rocprofv3 --pmc passes of
+    this same command) if it was collected for this kernel, blocking depth
+    and batch."""
+    if not os.path.exists(PMC_JSON):
         return None
-    with open(path) as f:
-        pmc = json.load(f)
-    if pmc.get("kb") == kb and pmc.get("batch") == batch:
-        return pmc
+    with open(PMC_JSON) as f:
+        e = json.load(f).get(pmc_key(wl_name, window, batch))
+    if e and e.get("kb") == kb and e.get("kernel") == kernel:
+        return e
     return None
 
 
+def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters, alpha,
+                 reps, step_s=None, ws=None):
+    """The dominant kernel alone (the Jacobi pass, K2), single stream, timed
+    with events on its launch stream: the per-launch duration rocprofv3
+    reports per dispatch.  Config 5: the level-0 plane, the pass that
+    dominates its solve."""
+    import torch
+    kb = hsflow.iters_per_launch(rows, cols, batch, window)
+    kernel = hsflow.jacobi_kernel_name(rows, cols, batch, window)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rws = ws if ws is not None else hsflow.alloc_workspace(rows, cols, batch, dev)
+    u = torch.empty((batch, rows, cols), dtype=torch.float32, device=dev)
+    v = torch.empty_like(u)
+    hsflow.gradients_device(I0, I1, rws, stream=stream)
+    launches_per_solve = -(-iters // kb)
+    # one stream so the per-launch duration is what rocprofv3 reports per
+    # dispatch (the batch split overlaps launches and would blur it)
+    hsflow.set_max_streams(1)
+    try:
+        hsflow.jacobi_device(rows, cols, batch, window, iters, alpha, u, v, rws, stream=stream)
+        torch.cuda.synchronize(dev)
+        ev0.record(stream)
+        for _ in range(reps):
+            hsflow.jacobi_device(rows, cols, batch, window, iters, alpha, u, v, rws,
+                                 stream=stream)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+    finally:
+        hsflow.set_max_streams(0)
+    k2_ms = ev0.elapsed_time(ev1) / (reps * launches_per_solve)
+    n_px = batch * rows * cols
+    # algorithmic bytes of one blocked pass: u, v in (the first pass of a
+    # solve reads none), packed gradients in, u, v out
+    pass_bytes = n_px * (PASS_BYTES_PER_PX - 8 / launches_per_solve)
+    achieved = pass_bytes / (k2_ms * 1e-3) / 1e9
+    naive = NAIVE_BYTES_PER_PX_ITER * n_px * iters / launches_per_solve / (k2_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": kernel, "avg_launch_ms": round(k2_ms, 5),
+            "iters_per_launch": kb, "launches_per_solve": launches_per_solve,
+            "algorithmic_bytes_per_launch": int(pass_bytes),
+            "algorithmic_B_per_px_pass": PASS_BYTES_PER_PX,
+            "naive_equiv_frac": round(naive / HBM_PEAK_GBPS, 4),
+            "naive_B_per_px_iter": NAIVE_BYTES_PER_PX_ITER,
+            "hbm_frac": None, "valu_frac": None}
+    pmc = pmc_for(wl_name, window, batch, kb, kernel)
+    if pmc is not None:
+        traffic = pmc["hbm_bytes_per_launch"]
+        roof["traffic"] = traffic
+        roof["traffic_over_algorithmic"] = round(traffic / pass_bytes, 3)
+        # physical HBM utilisation: the PMC bytes at the live launch time
+        roof["hbm_frac"] = round(traffic / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        roof["hbm_frac_vs_copy_peak"] = round(
+            traffic / (k2_ms * 1e-3) / 1e9 / COPY_PEAK_GBPS, 4)
+        if pmc.get("valu_insts_per_launch") and pmc.get("launch_cycles"):
+            # VALU issue at the guide's 2 cycles per wave64 instruction per
+            # SIMD (MI355X_MICROARCH.md constants table) over the launch's
+            # shader cycles (GRBM_GUI_ACTIVE / 8 XCDs)
+            roof["valu_frac"] = round(pmc["valu_insts_per_launch"] * 2.0 / 1024 /
+                                      pmc["launch_cycles"], 4)
+            roof["clock_ghz"] = pmc.get("clock_ghz")
+        roof["pmc_source"] = pmc.get("source")
+    del u, v
+    return roof
+
+
 # --------------------------------------------------------------- resident
-def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False,
-                 window=None):
+def resident_leg(wl_name, args, dev, world, rank, init_dist=None, window=None, batch=None,
+                 keep=False, roofline=True):
     """One workload, inputs resident in HBM: a step is one full solve of
-    `batch` pairs per rank (hipGraph replay).  Returns the leg's dict."""
+    `batch` pairs per rank (hipGraph replay).  Returns the leg's dict (and,
+    with keep, rank 0's timed (u, v) for cross-checks)."""
     import numpy as np
     import torch
     import hsflow
@@ -217,7 +363,7 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
     wl = dict(WORKLOADS[wl_name])
     rows, cols = wl["rows"], wl["cols"]
     iters = args.iters or wl["iters"]
-    batch = args.batch or wl["batch"]
+    batch = batch or args.batch or wl["batch"]
     levels = args.levels or wl.get("levels", 1)
     in_dtype = args.dtype or wl.get("dtype", "f32")
     window, alpha = (window or args.window), args.alpha
@@ -273,6 +419,11 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
         else:
             solve(stream)
 
+    # the output planes hold NaN when the timed steps start: the parity
+    # check below passes only if the replays themselves wrote (u, v)
+    u.fill_(float("nan"))
+    v.fill_(float("nan"))
+    torch.cuda.synchronize(dev)
     # the process group comes up after the first capture: no communicator
     # thread touches the device while a stream is capturing
     if init_dist is not None:
@@ -285,81 +436,34 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, with_cpu=False
     if rank == 0:
         golden = golden_entry(rows, cols, iters, window, levels, alpha)
         parity = parity_check(u[0].cpu().numpy(), v[0].cpu().numpy(), golden)
+        parity["outputs_nan_filled_before_timing"] = True
+    kept = (u.clone(), v.clone()) if (keep and rank == 0) else None
 
     px_all = sum(r * c for r, c in (hsflow.pyramid_level_size(rows, cols, l)
                                     for l in range(levels)))
     total_pairs = batch * world * args.steps
     value = total_pairs * px_all * iters / elapsed / 1e6
 
-    # ---- dominant-kernel roofline: K2 alone, events on its launch stream
-    kb = hsflow.iters_per_launch(rows, cols, batch, window)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # (config 5: K2 on the level-0 plane, the pass that dominates the solve)
-    rws = ws if levels == 1 else hsflow.alloc_workspace(rows, cols, batch, dev)
-    hsflow.gradients_device(I0, I1, rws, stream=stream)
-    launches_per_solve = -(-iters // kb)
-    reps = args.roofline_reps
-    # one stream so the per-launch duration is what rocprofv3 reports per
-    # dispatch (the batch split overlaps launches and would blur it)
-    hsflow.set_max_streams(1)
-    torch.cuda.synchronize(dev)
-    ev0.record(stream)
-    for _ in range(reps):
-        hsflow.jacobi_device(rows, cols, batch, window, iters, alpha, u, v, rws,
-                             stream=stream)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    hsflow.set_max_streams(0)
-    k2_ms = ev0.elapsed_time(ev1) / (reps * launches_per_solve)
-    n_px = batch * rows * cols
-    # algorithmic bytes = 28 B per pixel-iteration (read u, v,
-    # Ix, Iy, It; write u', v' in f32) x the pixel-iterations one launch
-    # performs -- fixed by the algorithm, whatever the blocking saves
-    bytes_per_launch = 28.0 * n_px * iters / launches_per_solve
-    achieved = bytes_per_launch / (k2_ms * 1e-3) / 1e9
-    # the HBM bytes one temporally-blocked pass cannot avoid: read u, v (f32)
-    # + packed gradients (4 B), write u, v; the first pass reads no u, v
-    compulsory = n_px * (8 + 4 + 8 - 8 / launches_per_solve)
-    compulsory_gbps = compulsory / (k2_ms * 1e-3) / 1e9
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-            "kernel": "hs_jacobi_wg_kernel", "avg_launch_ms": round(k2_ms, 5),
-            "iters_per_launch": kb, "launches_per_solve": launches_per_solve,
-            "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "algorithmic_B_per_px_iter": 28,
-            "compulsory_bytes_per_launch": int(compulsory),
-            "compulsory_frac": round(compulsory_gbps / HBM_PEAK_GBPS, 4),
-            "hbm_frac": None, "valu_frac": None, "step_hbm_frac": None}
-    pmc = pmc_for(wl_name, kb, batch) if levels == 1 and window == 5 else None
-    if pmc is not None:
-        traffic = pmc["hbm_bytes_per_launch"]
-        roof["traffic"] = traffic
-        # physical HBM utilisation: the PMC bytes at the live launch time
-        roof["hbm_frac"] = round(traffic / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-        if pmc.get("valu_insts_per_launch") and pmc.get("launch_cycles"):
-            # VALU issue cycles per SIMD / the launch's shader cycles (both
-            # from the profile; GRBM_GUI_ACTIVE / 8 XCDs = launch cycles)
-            roof["valu_frac"] = round(pmc["valu_insts_per_launch"] * VALU_CPI_4W /
-                                      SIMDS / pmc["launch_cycles"], 4)
-            roof["clock_ghz"] = pmc.get("clock_ghz")
-        if pmc.get("step_hbm_bytes_per_pass"):
-            # the timed solve: every pass's PMC bytes over the step time
-            step_bytes = pmc["step_hbm_bytes_per_pass"] * launches_per_solve * batch / pmc["batch"]
-            roof["step_hbm_frac"] = round(step_bytes / (elapsed / args.steps) / 1e9 /
-                                          HBM_PEAK_GBPS, 4)
-        roof["pmc_source"] = pmc.get("source")
+    step_kind = "hipGraph replay of one solve" if graph is not None else "eager solve"
+    del u, v, graph
+    roof = None
+    if roofline:
+        roof = roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
+                            alpha, args.roofline_reps, ws=ws if levels == 1 else None)
 
     leg = {"workload": f"{wl_name} {cols}x{rows}, {iters} it"
                        + (f"/level x {levels} levels" if levels > 1 else "")
-                       + f", ws {window}",
+                       + f", ws {window}" + (f", {batch} pair" + ("s" if batch > 1 else "")),
            "rows": rows, "cols": cols, "iters": iters, "window": window, "levels": levels,
            "input_dtype": in_dtype, "alpha": alpha, "pairs_per_gpu_per_step": batch,
-           "value": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "value": round(value, 1), "unit": "Mpix*iter/s",
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3),
            "pairs_per_s_resident": round(total_pairs / elapsed, 2),
-           "step": "hipGraph replay of one solve" if graph is not None else "eager solve",
-           "roofline": roof, "parity": parity}
-    del I0, I1, u, v, ws, pws, graph
+           "step": step_kind, "roofline": roof, "parity": parity}
+    del I0, I1, ws, pws
     torch.cuda.empty_cache()
+    if keep:
+        return leg, kept
     return leg
 
 
@@ -401,6 +505,8 @@ def config1_leg(dev, reps=20):
     u, v = hs.getFlow(I0, I1)  # warm
     ts = []
     for _ in range(reps):
+        u.fill(np.nan)
+        v.fill(np.nan)
         t = time.perf_counter()
         u, v = hs.getFlow(I0, I1)
         ts.append(time.perf_counter() - t)
@@ -412,9 +518,10 @@ def config1_leg(dev, reps=20):
     t = time.perf_counter()
     oracle.flow(I0.astype(np.float64), I1.astype(np.float64), 5, 100, 1.0, nthreads=1)
     cpu_ms = (time.perf_counter() - t) * 1e3
+    ok = bool(np.isfinite(u).all() and np.isfinite(v).all() and err <= PARITY_TOL)
     return {"workload": "KITTI 000050 crop 256x256 u8, ws 5, alpha 1, 100 it",
             "gpu_ms_host_api": round(ms, 3), "cpu_port_ms_1_thread": round(cpu_ms, 1),
-            "parity": {"golden": "crop256", "max_rel_err": err, "ok": bool(err <= PARITY_TOL)}}
+            "parity": {"golden": "crop256", "max_rel_err": err, "ok": ok}}
 
 
 # --------------------------------------------------------------- e2e
@@ -535,12 +642,20 @@ def _transport(world, dev):
     return f"{backend} ({dev.type} tensors)"
 
 
-def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
+def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, ref=None,
+               golden=None):
     """BASELINE config 4: a stream of n_pairs synthetic frame pairs held by
     rank 0, scattered one-per-rank round-robin (point-to-point over RCCL;
     gloo in the CPU tests), each rank's share solved in one batched call,
-    (u, v) gathered back to rank 0.  Timed end to end, max over ranks."""
+    (u, v) gathered back to rank 0.  Timed end to end, max over ranks.
+
+    Checked on rank 0 after the timed passes: pair 0 (seed 1000) against
+    `golden`, and pairs 0..k-1 bit for bit against `ref` = (u, v) of the
+    same seeds from the resident leg (frame pairs are independent and K2 is
+    bit-identical for any batch, split or blocking depth), so a mis-routed
+    or mis-ordered scatter or gather cannot pass."""
     import torch
+    import torch.distributed as dist
     import frame_parallel as fp
     import hsflow
 
@@ -569,6 +684,8 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
         out[0] = fp.run_stream_pipelined(stream, n, (rows, cols), torch.float32, solve_batch,
                                          dev, rank, world, chunks=chunks)
 
+    if world > 1:
+        dist.barrier()  # every rank's communicator is up before the first P2P call
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     steps = max(1, min(args.steps, 3))
     elapsed = timed_region(one_pass, sync, steps, 1, world, dev)
@@ -583,6 +700,18 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None):
         leg["gathered"] = len(res) if res is not None else 0
         leg["finite"] = bool(res is not None and all(bool(torch.isfinite(u).all())
                                                       for u, _ in res[:2]))
+        par = {"ok": bool(leg["finite"] and leg["gathered"] == n)}
+        if golden is not None and res:
+            g = parity_check(res[0][0].cpu().numpy(), res[0][1].cpu().numpy(), golden)
+            par["pair0"] = g
+            par["ok"] = par["ok"] and bool(g["ok"])
+        if ref is not None and res:
+            k = min(len(ref[0]), len(res))
+            same = [bool(torch.equal(res[j][0], ref[0][j]) and torch.equal(res[j][1], ref[1][j]))
+                    for j in range(k)]
+            par["bitwise_vs_resident"] = {"pairs": k, "identical": sum(same)}
+            par["ok"] = par["ok"] and all(same)
+        leg["parity"] = par
     return leg
 
 
@@ -593,6 +722,18 @@ def main():
     if bad:
         print(f"bench: refusing to run with diagnostic variables set: {bad}", file=sys.stderr)
         sys.exit(2)
+    action, world = world_from_env(args.gpus)
+    if action == "refuse":
+        print(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks; "
+              "refusing to report a line for the wrong GPU count", file=sys.stderr)
+        sys.exit(2)
+    if action == "launch":
+        sys.exit(launch_ranks(world))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        sys.exit(launch_check(world, rank))
+
     import torch
     import torch.distributed as dist
     import hsflow
@@ -601,9 +742,6 @@ def main():
         print(f"bench: {hsflow.LIB_PATH} is the probe build; rebuild the product library",
               file=sys.stderr)
         sys.exit(2)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # HSFLOW_BENCH_BACKEND=gloo + HSFLOW_BENCH_DEVICE=0: rehearse the N > 1
     # logic with several ranks on one GPU (diagnostics; the driver's runs
     # use RCCL, one GPU per rank)
@@ -623,7 +761,11 @@ def main():
 
     if args.mode == "stream":
         init_dist()
-        leg = stream_leg(args.workload, args, world, rank, dev)
+        golden = golden_entry(WORKLOADS[args.workload]["rows"], WORKLOADS[args.workload]["cols"],
+                              args.iters or WORKLOADS[args.workload]["iters"], args.window, 1,
+                              args.alpha) if rank == 0 else None
+        leg = stream_leg(args.workload, args, world, rank, dev, golden=golden)
+        status = 0
         if rank == 0:
             print(json.dumps({
                 "metric": "frame-pairs/s (config 4 stream: RCCL scatter + solve + gather)",
@@ -635,32 +777,46 @@ def main():
                 "config": {"workload": f"stream of {leg['pairs']} x {args.workload} pairs",
                            "parallelism": f"frame-parallel x{world}"},
                 "stream": leg}), flush=True)
+            status = 0 if leg["parity"]["ok"] else 3
         if world > 1:
             dist.destroy_process_group()
-        return
+        sys.exit(status)
     if args.mode == "bands":
         init_dist()
         return bands_mode(args, world, rank, dev)
 
     default_run = (args.workload == "1080p" and not args.iters and not args.batch and
-                   args.window == 5 and args.alpha == 1.0 and not args.levels)
+                   args.window == 5 and args.alpha == 1.0 and not args.levels and
+                   not args.dtype)
     if args.kb:
         hsflow.set_iters_per_launch(args.kb)
-    prim = resident_leg(args.workload, args, dev, world, rank, init_dist)
-    sec = None
+    keep = default_run and not args.no_stream
+    prim = resident_leg(args.workload, args, dev, world, rank, init_dist, keep=keep)
+    resident_ref = None
+    if keep:
+        prim, resident_ref = prim
+    sec = c5 = w3 = None
+    singles = {}
     if default_run and not args.no_secondary:
         sec = resident_leg("4k", args, dev, world, rank)
-    w3 = None
     if default_run and not args.no_w3:
         # windowSize 5 is the headline, report 3 (north_star) too
         w3 = resident_leg("1080p", args, dev, world, rank, window=3)
+    if default_run and not args.no_8k:
+        c5 = resident_leg("8k", args, dev, world, rank)
+    if default_run and not args.no_single:
+        # configs[1] / configs[2] as stated: one pair per solve (main.cpp:97-98)
+        for wl in ("1080p", "4k"):
+            singles[wl] = resident_leg(wl, args, dev, world, rank, batch=1)
     stream_peak = hbm_stream_peak(dev) if rank == 0 else None
     e2e = None
     if not args.no_e2e and args.workload != "8k" and rank == 0:
         e2e = e2e_leg(args.workload, args, dev)
     strm = None
-    if not args.no_stream and args.workload == "1080p":
-        strm = stream_leg("1080p", args, world, rank, dev)
+    if default_run and not args.no_stream:
+        golden = golden_entry(1080, 1920, 300, 5, 1, 1.0) if rank == 0 else None
+        strm = stream_leg("1080p", args, world, rank, dev, ref=resident_ref, golden=golden)
+    del resident_ref
 
     c1 = config1_leg(dev) if (default_run and rank == 0) else None
     cpu = cpu_all = None
@@ -676,6 +832,10 @@ def main():
             # the CPU line per config -- 4K on 1 thread, bounded
             sec["cpu_baseline"] = cpu_baseline(sec["rows"], sec["cols"], args.window,
                                                args.alpha, args.cpu_iters or 20)
+        if c5 is not None:
+            # the 8K level-0 plane, 1 thread, 4 iterations (~6 s)
+            c5["cpu_baseline"] = cpu_baseline(c5["rows"], c5["cols"], args.window,
+                                              args.alpha, args.cpu_iters or 4)
 
     status = 0
     if rank == 0:
@@ -704,39 +864,43 @@ def main():
         }
         line["config"]["parallelism"] = f"frame-parallel x{world}"
         line["config"]["iters_per_launch"] = prim["roofline"]["iters_per_launch"]
+        line["config"]["kernel"] = prim["roofline"]["kernel"]
         if e2e is not None:
             line.update(e2e)
+        keys = ("workload", "value", "unit", "ms_per_step", "pairs_per_s_resident", "roofline",
+                "parity", "cpu_baseline")
         if sec is not None:
-            line["secondary"] = {k: sec[k] for k in ("workload", "value", "ms_per_step",
-                                                     "pairs_per_s_resident", "roofline",
-                                                     "parity", "cpu_baseline") if k in sec}
-            line["secondary"]["unit"] = "Mpix*iter/s"
+            line["secondary"] = {k: sec[k] for k in keys if k in sec}
+        if c5 is not None:
+            line["config5"] = {k: c5[k] for k in keys if k in c5}
+        if singles:
+            line["single_pair"] = {wl: {k: s[k] for k in keys if k in s}
+                                   for wl, s in singles.items()}
         if c1 is not None:
             line["config1"] = c1
         if w3 is not None:
-            line["window3"] = {k: w3[k] for k in ("workload", "value", "ms_per_step",
-                                                  "pairs_per_s_resident", "parity")}
-            line["window3"]["unit"] = "Mpix*iter/s"
-            line["window3"]["avg_launch_ms"] = w3["roofline"]["avg_launch_ms"]
+            line["window3"] = {k: w3[k] for k in keys if k in w3}
         if stream_peak is not None:
-            # also against a measured stream-copy peak -- the
-            # guide's float4 copy (6.29 TB/s, the higher and so stricter
-            # one) next to torch's copy_ measured here
-            for leg in (line["roofline"], line.get("secondary", {}).get("roofline")):
-                if leg is not None:
-                    leg["copy_peak_gbps"] = COPY_PEAK_GBPS
-                    leg["torch_copy_gbps"] = stream_peak
-                    if leg.get("traffic"):
-                        leg["hbm_frac_vs_copy_peak"] = round(
-                            leg["traffic"] / (leg["avg_launch_ms"] * 1e-3) / 1e9 /
-                            max(COPY_PEAK_GBPS, stream_peak), 4)
+            line["torch_copy_gbps"] = stream_peak
         if strm is not None:
             line["stream"] = strm
+        # one verdict per BASELINE config
+        legs = {"configs[0]": [c1], "configs[1]": [prim, singles.get("1080p"), w3],
+                "configs[2]": [sec, singles.get("4k")], "configs[3]": [strm],
+                "configs[4]": [c5]}
+        verdict = {}
+        for name, ls in legs.items():
+            ps = [l["parity"] for l in ls if l is not None and l.get("parity") is not None]
+            oks = [p["ok"] for p in ps if p.get("ok") is not None]
+            verdict[name] = (all(oks) if oks else None)
+        line["parity_all"] = {"ok": all(v is not False for v in verdict.values()),
+                              "configs": verdict}
         print(json.dumps(line), flush=True)
-        for leg in (prim, sec, w3, c1):
-            if leg is not None and leg["parity"] is not None and leg["parity"]["ok"] is False:
-                print(f"bench: PARITY FAILURE on {leg['workload']}: {leg['parity']}",
-                      file=sys.stderr)
+        for leg in (prim, sec, w3, c5, c1, strm, *singles.values()):
+            if leg is not None and leg.get("parity") is not None and \
+                    leg["parity"].get("ok") is False:
+                print(f"bench: PARITY FAILURE on {leg.get('workload', 'stream')}: "
+                      f"{leg['parity']}", file=sys.stderr)
                 status = 3
     if world > 1:
         dist.destroy_process_group()
@@ -788,6 +952,7 @@ def bands_mode(args, world, rank, dev):
     elapsed = timed_region(one, lambda: torch.cuda.synchronize(dev), args.steps, args.warmup,
                            world, dev)
     px_all = sum(r * c for r, c in p.sizes)
+    status = 0
     if rank == 0:
         u, v = res[0]
         golden = golden_entry(rows, cols, iters, args.window, levels, args.alpha)
@@ -805,8 +970,11 @@ def bands_mode(args, world, rank, dev):
                        else "after every chunk",
                        "parallelism": f"row bands x{world}"},
             "parity": parity}), flush=True)
+        status = 3 if parity.get("ok") is False else 0
     if world > 1:
         dist.destroy_process_group()
+    if status:
+        sys.exit(status)
 
 
 def cpu_baseline(rows, cols, window, alpha, cpu_iters, threads=1):

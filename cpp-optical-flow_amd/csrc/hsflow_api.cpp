@@ -44,10 +44,32 @@ namespace {
 
 thread_local std::string g_err;  // errors from calls without a context
 int g_kb_override = 0;
-// Jacobi pass kernel (hsflow_set_jacobi_kernel): 0 = automatic, 2 = K2 tiles,
-// one launch per pass -- both run K2 (the persistent K2p and the streaming
-// K3 alternatives measured slower and were retired)
+// Jacobi pass kernel (hsflow_set_jacobi_kernel): 0 = automatic (K4 strips
+// where built, else K2), 2 = K2 tiles everywhere, 4 = K4 where built
 int g_kernel_override = 0;
+// K4 rows per segment (hsflow_set_strip_rows): 0 = automatic
+int g_strip_rows = 0;
+// K4 passes alternate their streaming direction (hsflow_set_strip_options)
+int g_strip_dir_alt = 1;
+
+// Kernel and blocking depth of a launch's passes.  K4 (streaming strips)
+// runs the full-depth passes when it is built for the window's default
+// depth and -- automatic choice -- its waves fill the chip (launches too
+// small for it keep K2's tiles, whose depth adapts to the fill);
+// hsflow_set_jacobi_kernel(4) forces it wherever it is built.
+struct PassPlan {
+    int kb;
+    bool strip;
+};
+
+bool strip_use(int window, int rows, int cols, int batch) {
+    const int kb = hsflow::default_kb(window);
+    if (g_kernel_override == 2 || window > 9 || !hsflow::strip_supported(window, kb)) return false;
+    if (g_kb_override > 0 && g_kb_override != kb) return false;
+    if (g_kernel_override == 4) return true;
+    return rows > 0 && cols > 0 && batch > 0 &&
+           hsflow::strip_fills(window, kb, rows, cols, batch, 8 * hsflow::device_cus());
+}
 
 int fail(hsflow_ctx *ctx, int code, const char *fmt, ...) {
     char buf[512];
@@ -135,13 +157,18 @@ bool device_dtype_ok(int dtype) {
 
 // `batch`: every pair in flight at once (the whole batch, also when it is
 // split over side streams); 0 = shape unknown (no fill adjustment)
-int pick_kb(int window, bool need_f32, int rows = 0, int cols = 0, int batch = 0) {
-    if (window > 9) return 1;
+PassPlan plan_passes(int window, bool need_f32, int rows = 0, int cols = 0, int batch = 0) {
+    if (window > 9) return {1, false};
+    if (strip_use(window, rows, cols, batch)) return {hsflow::default_kb(window), true};
     if (g_kb_override > 0 && hsflow::kb_supported(window, g_kb_override, need_f32))
-        return g_kb_override;
+        return {g_kb_override, false};
     int kb = hsflow::fill_kb(window, hsflow::default_kb(window), rows, cols, batch);
     while (kb > 1 && !hsflow::kb_supported(window, kb, need_f32)) kb /= 2;
-    return kb;
+    return {kb, false};
+}
+
+int pick_kb(int window, bool need_f32, int rows = 0, int cols = 0, int batch = 0) {
+    return plan_passes(window, need_f32, rows, cols, batch).kb;
 }
 
 // Per-thread, per-device side streams for splitting a batch: each sub-batch
@@ -180,13 +207,7 @@ struct SidePool {
 
 int g_split_override = 0;
 
-int max_split() {
-    static const int n = [] {  // probe build: HSFLOW_STREAMS
-        int k = hsflow::probe_env("HSFLOW_STREAMS", 2);
-        return k < 1 ? 1 : (k > 16 ? 16 : k);
-    }();
-    return g_split_override > 0 ? g_split_override : n;
-}
+int max_split() { return g_split_override > 0 ? g_split_override : 2; }
 
 SidePool *side_pool(int need) {
     // one pool per device and thread: a thread that alternates devices keeps
@@ -267,8 +288,20 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         }
         return HSFLOW_OK;
     }
-    const int kb = pick_kb(window, maybe_f32, rows, cols, fill_batch);
+    const PassPlan plan = plan_passes(window, maybe_f32, rows, cols, fill_batch);
+    const int kb = plan.kb;
     const int passes = (iters + kb - 1) / kb;
+    // K4 for the full-depth passes (two waves per SIMD: 8 per CU), K2 for a
+    // shorter last pass -- identical bits either way
+    const bool strip = plan.strip;
+    // K4 segment height from every pair in flight (the halves of a split
+    // batch run concurrently and share the chip's slots)
+    int strip_rows = g_strip_rows;
+    if (strip && strip_rows <= 0) {
+        int nseg = 0, nstrips = 0;
+        strip_rows = hsflow::strip_seg_rows(window, kb, rows, cols, fill_batch,
+                                            8 * hsflow::device_cus(), &nseg, &nstrips, 0);
+    }
     JacobiArgs a{};
     a.rows = rows;
     a.cols = cols;
@@ -280,8 +313,6 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
     a.gy = w.gy;
     a.gt = w.gt;
     a.flags = w.flags;
-    static const int ablate = hsflow::probe_env("HSFLOW_ABLATE", 0);
-    a.ablate = ablate;  // the product kernels ignore it (compiled out)
     // pass p writes the caller's buffers iff (passes-1-p) is even, so the
     // last pass always lands in (u, v)
     auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };
@@ -304,7 +335,10 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         a.v_in = src_v;
         a.u_out = dst_is_user(pass) ? u : w.u2;
         a.v_out = dst_is_user(pass) ? v : w.v2;
-        hipError_t e = hsflow::launch_jacobi(a, window, kb, s);
+        a.strip_up = g_strip_dir_alt ? (pass & 1) : 0;
+        hipError_t e = (strip && a.iters == kb)
+                           ? hsflow::launch_jacobi_strip(a, window, kb, strip_rows, s)
+                           : hsflow::launch_jacobi(a, window, kb, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "jacobi launch");
         src_u = a.u_out;
         src_v = a.v_out;
@@ -607,7 +641,9 @@ extern "C" {
 
 int hsflow_version(void) { return HSFLOW_VERSION; }
 
-int hsflow_build_flags(void) { return hsflow::kProbeBuild ? HSFLOW_BUILD_PROBE : 0; }
+// No diagnostic build exists any more (the environment-honouring probe build
+// of round 2 was retired with its switches); kept for ABI stability.
+int hsflow_build_flags(void) { return 0; }
 
 const char *hsflow_status_string(int status) {
     switch (status) {
@@ -678,9 +714,24 @@ int hsflow_set_iters_per_launch(int k) {
 }
 
 int hsflow_set_jacobi_kernel(int k) {
-    if (k != 0 && k != 2) return HSFLOW_ERR_ARG;
+    if (k != 0 && k != 2 && k != 4) return HSFLOW_ERR_ARG;
     g_kernel_override = k;
     return HSFLOW_OK;
+}
+
+int hsflow_set_strip_options(int seg_rows, int alternate) {
+    if (seg_rows < 0 || seg_rows > kMaxRows || alternate < 0 || alternate > 1)
+        return HSFLOW_ERR_ARG;
+    g_strip_rows = seg_rows;
+    g_strip_dir_alt = alternate;
+    return HSFLOW_OK;
+}
+
+const char *hsflow_jacobi_kernel_name(int rows, int cols, int batch, int window) {
+    if (window < 1 || window > HSFLOW_MAX_WINDOW || !sizes_ok(rows, cols, batch)) return "";
+    if (window > 9) return "hs_jacobi_generic_kernel";
+    if (plan_passes(window, true, rows, cols, batch).strip) return "hs_jacobi_strip_kernel";
+    return window >= 3 ? "hs_jacobi_wg_kernel" : "hs_jacobi_kernel";
 }
 
 int hsflow_set_max_streams(int n) {

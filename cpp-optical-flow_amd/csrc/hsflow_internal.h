@@ -6,25 +6,6 @@
 
 namespace hsflow {
 
-// Diagnostic environment switches (HSFLOW_K2_TL, HSFLOW_ABLATE, ...) exist
-// only in the probe build (`make probe` -> libhsflow_probe.so, compiled with
-// -DHSFLOW_PROBE).  The product library never reads the environment, so no
-// variable can change the work a caller (or bench.py) times.
-#ifdef HSFLOW_PROBE
-constexpr bool kProbeBuild = true;
-#else
-constexpr bool kProbeBuild = false;
-#endif
-inline int probe_env(const char *name, int dflt) {
-#ifdef HSFLOW_PROBE
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
-#else
-    (void)name;
-    return dflt;
-#endif
-}
-
 // Arguments of one Jacobi launch (hornSchunck.cpp:56-74 x `iters`).
 struct JacobiArgs {
     int rows, cols, batch;
@@ -37,16 +18,8 @@ struct JacobiArgs {
     const uint32_t *gpack;     // packed exact integer gradients
     const float *gx, *gy, *gt; // f32 gradients (non-integral inputs)
     const uint32_t *flags;     // per pair: 0 -> gpack valid, else f32 planes
-    int ablate;                // probe build only (HSFLOW_ABLATE): 1 = no
-                               // iterations (memory only), 2 = no memory
-                               // traffic (descriptors of size 0); always 0
-                               // in the product library
-    int band_w;                // K2 workgroup kernel: tile-column band width
-                               // of the tile order (0 = row-major; launcher)
-#ifdef HSFLOW_DEV_TRACE
-    long trace_base;           // development builds: first trace record of
-                               // this launch (-1: off)
-#endif
+    int seg_rows;              // K4 strip kernel: output rows per segment
+    int strip_up;              // K4: stream this pass upwards (odd passes)
 };
 
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
@@ -61,6 +34,15 @@ hipError_t launch_bgr2gray(const uint8_t *bgr, int rows, int cols, int batch,
                            uint8_t *gray, hipStream_t s);
 hipError_t launch_upflow(const float *uc, const float *vc, int rc, int cc, float *u,
                          float *v, int rows, int cols, int batch, hipStream_t s);
+// K4 (hsflow_strips.hip): the streaming pass for the (window, KB) pairs it
+// is built for; `slots` = waves the chip holds at its occupancy
+bool strip_supported(int W, int KB);
+hipError_t launch_jacobi_strip(JacobiArgs a, int W, int KB, int seg_rows, hipStream_t s);
+int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int *nseg,
+                   int *nstrips, int override_rows);
+bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots);
+// compute units of the current device (cached per device)
+int device_cus();
 int default_kb(int W);
 // default_kb adjusted for launches that do not fill one round of slots
 int fill_kb(int W, int kb, int rows, int cols, int batch);

@@ -2,63 +2,38 @@
 //
 // Replaces the numeric body of HornSchunckOF/hornSchunck.cpp:19-75 (the
 // reference runs it as ~15 OpenCV full-image float64 passes per iteration,
-// SURVEY.md §2.1).  Two kernels:
+// SURVEY.md §2.1).
 //
-//  K1 hs_gradients_kernel   hornSchunck.cpp:19-41, once per pair.
-//     Sobel Ix, Iy on I0 (reflect-101) and It = I1 - I0.  For 8-bit-valued
-//     inputs these are small integers (|Ix|,|Iy| <= 1020, |It| <= 255) and are
-//     packed EXACTLY into one 32-bit word (11+11+9 bit two's complement), so
-//     the Jacobi loop streams 4 B of gradients per pixel instead of 12.
-//     Non-integral f32 inputs set a per-pair flag; K2 then takes an f32-plane
-//     branch for that pair (same launch, shorter regions).
+//  K1  hs_gradients_kernel   hornSchunck.cpp:19-41, once per pair.
+//      Sobel Ix, Iy on I0 (reflect-101) and It = I1 - I0.  For 8-bit-valued
+//      inputs these are small integers (|Ix|,|Iy| <= 1020, |It| <= 255) and
+//      are packed EXACTLY into one 32-bit word (11+11+9 bit two's
+//      complement), so a Jacobi pass streams 4 B of gradients per pixel
+//      instead of 12.  Non-integral inputs set a per-pair flag; the Jacobi
+//      kernels then read that pair's f32 gradient planes.
 //
-//  K2 hs_jacobi_kernel      hornSchunck.cpp:56-74, the hot loop.
-//     Register-resident, temporally blocked stencil: one wavefront owns a
-//     64-column x RH-row region of (u, v, packed gradients) held in VGPRs
-//     (lane = column, unrolled row arrays), runs KB Jacobi iterations on it
-//     without touching memory (horizontal box sums by cross-lane permutes,
-//     vertical sums by a W-deep register ring, in-place row update), and
-//     writes back the interior (64 - KB(W-1)) x (RH - KB(W-1)) tile.  Halo =
-//     KB * anchor extents; outside the image u = v = 0 (BORDER_CONSTANT,
-//     hornSchunck.cpp:60-61) is re-imposed after every iteration.  No LDS, no
-//     barriers: every wave is independent.  Ping-pong u/v buffers between
-//     launches.  Results are bit-identical for every KB (same per-pixel
-//     operation sequence), which the tests check.
+//  K2  hs_jacobi_wg_kernel   hornSchunck.cpp:56-74, windows 3..9: one pass
+//      of KB Jacobi iterations on register-resident 128-column tiles (eight
+//      stacked waves per workgroup, boundary rows exchanged through LDS,
+//      temporal halo KB*(W-1) rows and columns).  Runs the passes K4 does
+//      not (launches too small to fill the chip with K4 segments, other
+//      windows and depths, a shorter last pass).  K4 (hsflow_strips.hip)
+//      streams the full-depth passes of windows 3 and 5 and gives the same
+//      bits.
 //
-//  K2g hs_jacobi_generic_kernel   any window up to HSFLOW_MAX_WINDOW, one
-//     iteration per launch, direct sums from L1/L2.  Used for windows > 9.
+//  K2w hs_jacobi_kernel      windows 1 and 2: one wave per 64-column region.
+//  K2g hs_jacobi_generic_kernel  any window up to HSFLOW_MAX_WINDOW, one
+//      iteration per launch (windows > 9).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "hsflow_internal.h"
 #include "hsflow_device.h"
 
-#ifdef HSFLOW_DEV_TRACE
-#include <atomic>
-// Development builds only: per-workgroup phase timestamps of the K2
-// workgroup kernel (s_memrealtime, 100 MHz) -- entry, operator set-up done,
-// iterations done, stores issued -- plus the hardware ids, written by lane
-// 0..5 of wave 0 with vector buffer stores.  scripts/k2_trace.py reads them.
-namespace hsflow {
-constexpr long kTraceCap = 1L << 18;  // workgroup records
-__device__ unsigned long long g_k2_trace[kTraceCap * 6];
-static std::atomic<long> g_trace_next{0};
-}  // namespace hsflow
-extern "C" __attribute__((visibility("default"))) int hsflow_dev_trace_read(
-    void *host, size_t max_records, size_t *n) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    long cnt = hsflow::g_trace_next.exchange(0);
-    size_t m = (size_t)(cnt < hsflow::kTraceCap ? cnt : hsflow::kTraceCap);
-    if (m > max_records) m = max_records;
-    *n = m;
-    if (m && hipMemcpyFromSymbol(host, HIP_SYMBOL(hsflow::g_k2_trace), m * 48, 0,
-                                 hipMemcpyDeviceToHost) != hipSuccess)
-        return -1;
-    return 0;
-}
-#endif
 
 namespace hsflow {
 
@@ -385,11 +360,7 @@ constexpr bool wg_double_buffer(int W) { return W <= 5; }
 // (32 KB exchange + 48 KB T plane each)
 // Any slab taller than the all-register height wg_rows(W) keeps T in LDS.
 // (w = 3 keeps the double-buffered exchange: 2 boundary rows, 32 KB + 44 KB.)
-#ifdef HSFLOW_DEV_TL_ALWAYS  // development: T plane in LDS at any slab height (w = 5)
-constexpr bool wg_tlds(int W, int RW) { return W == 5 || RW > wg_rows(W); }
-#else
 constexpr bool wg_tlds(int W, int RW) { return RW > wg_rows(W); }
-#endif
 constexpr int wg_nbuf(int W, int RW) {
     return (wg_double_buffer(W) && !(W >= 4 && wg_tlds(W, RW))) ? 2 : 1;
 }
@@ -432,11 +403,7 @@ __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
                                         float2 *tpl, int logical);
 
 // 4 waves per SIMD (<= 128 VGPRs): two 8-wave workgroups per CU
-#ifdef HSFLOW_DEV_WAVES  // development: other occupancy targets
-constexpr int kK2Waves = HSFLOW_DEV_WAVES;
-#else
 constexpr int kK2Waves = 4;
-#endif
 template <int W, int KB, int RW, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, kK2Waves) void hs_jacobi_wg_kernel(const JacobiArgs p) {
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
@@ -475,21 +442,9 @@ __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
     const int pair = logical / ntile;
     const int tile = logical - pair * ntile;
     if (pair >= p.batch) return;  // whole workgroup: uniform
-    // Tile order inside a pair: row-major, or (band_w > 0) bands of band_w
-    // tile columns walked row-major one band after the other, so that a
-    // tile's upper neighbour was loaded band_w (not tiles_x) workgroups
-    // earlier and its halo rows are still in the XCD's L2.
-    int ty, tx;
-    if (p.band_w > 0 && p.band_w < p.tiles_x) {
-        const int band_tiles = p.band_w * p.tiles_y;
-        const int band = tile / band_tiles, in = tile - band * band_tiles;
-        const int bw = min(p.band_w, p.tiles_x - band * p.band_w);
-        ty = in / bw;
-        tx = band * p.band_w + (in - ty * bw);
-    } else {
-        ty = tile / p.tiles_x;
-        tx = tile - ty * p.tiles_x;
-    }
+    // tiles of a pair in row-major order
+    const int ty = tile / p.tiles_x;
+    const int tx = tile - ty * p.tiles_x;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int cols = p.cols;
@@ -507,11 +462,7 @@ __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
     // (same tiles, same operator, any blocking depth).
     const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols &&
                           ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows;
-#ifdef HSFLOW_DEV_NOFLAG  // development ablation: no flags read (packed only)
-    const bool g32 = false;
-#else
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
-#endif
     if (g32) {
         if ((cols & 1) == 0)
             wg_body<W, KB, RW, NW, SB, true, true, true>(p, xch, tpl, tx, ty, wv, lane, pbase,
@@ -548,12 +499,6 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     // sinking the two parity bodies' identical load and store code into the
     // shared path (which costs ~50 spilled VGPRs at 11-row slabs)
     asm volatile("; slab parity %0 begin" ::"n"(PAR));
-#ifdef HSFLOW_DEV_PRIO_SETUP  // development: raised wave priority for loads + set-up
-    __builtin_amdgcn_s_setprio(2);
-#endif
-#ifdef HSFLOW_DEV_TRACE
-    const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
-#endif
     constexpr int A = W - W / 2 - 1, AR = W - 1 - A;
     constexpr int HL = KB * A, HR = KB * AR;
     constexpr int HLc = HL + (HL & 1), HRc = HR + (HR & 1);
@@ -574,22 +519,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         rowmask |= (uint64_t)((unsigned)(r0 + r) < (unsigned)p.rows) << r;
 
     constexpr int kOOB = 0x7FFFFFF0;
-#ifdef HSFLOW_DEV_LAUX_UV  // development: cache policy of the u, v slab loads
-    constexpr int LAUX_UV = HSFLOW_DEV_LAUX_UV;
-#else
-    constexpr int LAUX_UV = 0;
-#endif
-#ifdef HSFLOW_DEV_LAUX_G  // development: cache policy of the packed-gradient loads
-    constexpr int LAUX_G = HSFLOW_DEV_LAUX_G;
-#else
-    constexpr int LAUX_G = 0;
-#endif
-    const int ablate = kProbeBuild ? p.ablate : 0;  // compiled out of the product
-#ifdef HSFLOW_DEV_NOMEM  // development ablation: loads and stores out of range
-    const int nbytes = 0;
-#else
-    const int nbytes = ablate == 2 ? 0 : plane_bytes;
-#endif
+    const int nbytes = plane_bytes;
     const auto u_rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase), 0, p.u_in ? nbytes : 0,
         0x00020000);
@@ -627,8 +557,8 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
             if constexpr (X2) {
                 const int o = (!EDGE || (((rowmask >> r) & 1ull) && ce))
                                   ? off0 + r * cols * 4 : kOOB;
-                const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, LAUX_UV);
-                const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, LAUX_UV);
+                const u2v a = __builtin_amdgcn_raw_buffer_load_b64(u_rs, o, 0, 0);
+                const u2v b = __builtin_amdgcn_raw_buffer_load_b64(v_rs, o, 0, 0);
                 U[r] = f2v{__uint_as_float(a.x), __uint_as_float(a.y)};
                 V[r] = f2v{__uint_as_float(b.x), __uint_as_float(b.y)};
                 if constexpr (G32) {
@@ -639,7 +569,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                     iye = __uint_as_float(gy2.x); iyo = __uint_as_float(gy2.y);
                     ite = __uint_as_float(gt2.x); ito = __uint_as_float(gt2.y);
                 } else {
-                    const u2v g = __builtin_amdgcn_raw_buffer_load_b64(gp_rs, o, 0, LAUX_G);
+                    const u2v g = __builtin_amdgcn_raw_buffer_load_b64(gp_rs, o, 0, 0);
                     unpack_grad(g.x, ixe, iye, ite);
                     unpack_grad(g.y, ixo, iyo, ito);
                 }
@@ -675,15 +605,6 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         }
     }
 
-#ifdef HSFLOW_DEV_TRACE
-    const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef HSFLOW_DEV_PRIO_SETUP
-    __builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef HSFLOW_DEV_PRIO_ITER  // development: iterating waves above loading ones
-    __builtin_amdgcn_s_setprio(HSFLOW_DEV_PRIO_ITER);
-#endif
     const float inv = p.inv_w2;
     const f2v invv = {inv, inv};
     auto t_row = [&](int y) -> f2v {
@@ -702,11 +623,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         hv = f2v{c, d};
     };
 
-#ifdef HSFLOW_DEV_NOIT  // development ablation: no iterations
-    const int n_it = 0 * p.iters;
-#else
-    const int n_it = ablate == 1 ? 0 : p.iters;
-#endif
+    const int n_it = p.iters;
     // The vertical sums follow the parity of the image row (PAR = parity
     // of slab row 0), so every slab height, blocking depth and kernel
     // adds in the same order.  w = 5: pair sums Q(t) = h(t) + h(t+1) at
@@ -768,9 +685,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
             xch[par][wv][AR + k][0][lane] = make_float2(hbu[k].x, hbu[k].y);
             xch[par][wv][AR + k][1][lane] = make_float2(hbv[k].x, hbv[k].y);
         }
-#ifndef HSFLOW_DEV_NOBAR  // development ablation: timing without the barriers
         __syncthreads();
-#endif
 
         // 2. sweep slab rows t = -A .. RW+AR-1 through a ring of horizontal
         //    sums (hu, hv) and vertical pair sums q(t) = h(t) + h(t+1)
@@ -907,21 +822,13 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
         }
         // single-buffered exchange: the neighbours' reads of this iteration
         // must finish before the next iteration's publish overwrites them
-#ifndef HSFLOW_DEV_NOBAR
         if constexpr (!LAST && wg_nbuf(W, RW) == 1) __syncthreads();
-#endif
     };
     int it = 0;
     for (; it + 1 < n_it; ++it) iteration(it, std::false_type{});
-#ifdef HSFLOW_DEV_PRIO_LAST  // development: raised wave priority for the storing sweep
-    __builtin_amdgcn_s_setprio(2);
-#endif
     if (it < n_it) iteration(it, std::true_type{});
 
     asm volatile("; slab parity %0 sweep end" ::"n"(PAR));
-#ifdef HSFLOW_DEV_TRACE
-    const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
-#endif
     // no iteration ran (iters = 0): the loaded state is the output
     if (n_it == 0) {
         const int c4 = launder(gce * 4);
@@ -930,26 +837,6 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
 #pragma unroll
         for (int r = 0; r < RW; ++r) store_row(r, vo_e, vo_o);
     }
-#ifdef HSFLOW_DEV_TRACE
-    {
-        const uint64_t tr3 = __builtin_amdgcn_s_memrealtime();
-        const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
-        const long rec = p.trace_base +
-                         (long)(pbase / ((size_t)p.rows * cols)) * (p.tiles_x * p.tiles_y) +
-                         (long)ty * p.tiles_x + tx;
-        const uint64_t meta = (uint64_t)hwid | ((uint64_t)xcc << 32);
-        const uint64_t tile = (uint64_t)(unsigned)tx | ((uint64_t)(unsigned)ty << 16) |
-                              ((uint64_t)blockIdx.x << 32);
-        const uint64_t val = lane == 0 ? tr0 : lane == 1 ? tr1 : lane == 2 ? tr2
-                           : lane == 3 ? tr3 : lane == 4 ? meta : tile;
-        const bool on = wv == 0 && lane < 6 && p.trace_base >= 0 && rec < kTraceCap;
-        const auto trs = __builtin_amdgcn_make_buffer_rsrc((void *)g_k2_trace, 0,
-                                                           (int)(kTraceCap * 48), 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)val, (uint32_t)(val >> 32)}, trs,
-                                              on ? (int)((rec * 6 + lane) * 8) : kOOB, 0, 0);
-    }
-#endif
     asm volatile("; slab parity %0 end" ::"n"(PAR));
 }
 
@@ -1027,16 +914,9 @@ static hipError_t launch_jacobi_t(JacobiArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// K2 variant (HSFLOW_K2, probe build only): 0 = per-wave regions
-// (hs_jacobi_kernel) for every window; otherwise the workgroup kernel.
-static int k2_variant() {
-    static const int v = probe_env("HSFLOW_K2", 88);
-    return v;
-}
-
 // windows 3..9; w = 1, 2 keep the per-wave kernel (a 1-column halo makes
 // it fast already: 920 k Mpix*iter/s at w = 2), wider windows the generic one
-static bool uses_wg_kernel(int W) { return W >= 3 && W <= 9 && k2_variant() != 0; }
+static bool uses_wg_kernel(int W) { return W >= 3 && W <= 9; }
 
 // Temporal-blocking depth per window (overridable through
 // hsflow_set_iters_per_launch).  The workgroup kernel (W = 3, 5) takes
@@ -1072,19 +952,21 @@ bool kb_supported(int W, int KB, bool need_f32) {
     return need_f32 ? kb_ok_f32(W, KB) : kb_ok_packed(W, KB);
 }
 
-// compute units of the current device (cached per device id)
-static int device_cus() {
-    static int per_dev[64];
+// compute units of the current device (cached per device id; relaxed atomics:
+// concurrent solves from several host threads may fill an entry together,
+// with the same value)
+int device_cus() {
+    static std::atomic<int> per_dev[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (per_dev[dev] == 0) {
-        int cus = 0;
+    int cus = per_dev[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                 hipSuccess || cus <= 0)
             cus = 256;
-        per_dev[dev] = cus;
+        per_dev[dev].store(cus, std::memory_order_relaxed);
     }
-    return per_dev[dev];
+    return cus;
 }
 
 // workgroups of a workgroup-kernel launch with RW-row slabs (8 waves)
@@ -1126,21 +1008,8 @@ static hipError_t launch_jacobi_wg(JacobiArgs a, hipStream_t s) {
     a.tiles_y = (a.rows + OY - 1) / OY;
     const long ntiles = (long)a.tiles_x * a.tiles_y;
     dim3 grd((unsigned)ntiles, (unsigned)a.batch, 1);
-    // probe build only: HSFLOW_K2_BAND = tile order in bands of that many
-    // tile columns (0: row-major); HSFLOW_EXTRA_LDS = bytes of unused dynamic
-    // LDS per workgroup (lowers the workgroups per CU, occupancy probes)
-    static const int band_env = probe_env("HSFLOW_K2_BAND", 0);
-    a.band_w = band_env;
-    static const unsigned extra_lds = (unsigned)probe_env("HSFLOW_EXTRA_LDS", 0);
-#ifdef HSFLOW_DEV_TRACE
-    {
-        static const bool on = getenv("HSFLOW_DEV_TRACE_ON") != nullptr;
-        const long n = (long)ntiles * a.batch;
-        a.trace_base = on ? g_trace_next.fetch_add(n) : -1;
-    }
-#endif
-    hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW, SB>), grd, dim3(NW * 64),
-                       extra_lds, s, a);
+    hipLaunchKernelGGL((hs_jacobi_wg_kernel<W, KB, RW, NW, SB>), grd, dim3(NW * 64), 0, s,
+                       a);
     return hipGetLastError();
 }
 
@@ -1163,15 +1032,13 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     // Taller slabs with the T plane in LDS (wg_rows_tl): w = 5, 11 rows
     // (88 x 128 region), single-buffered exchange: same box, 1080p x 8 /
     // 4K x 2, 1.011 M / 1.072 M -> 1.032 M / 1.089 M Mpix*iter/s (12 rows
-    // spill).  Probe build: HSFLOW_K2_TL=0 keeps the all-register slabs everywhere,
-    // =1 uses the taller ones for every window that has them; default w = 5
-    // and w = 6 (8 -> 10 rows: 1080p 782 k -> 859 k, 4K 793 k -> 891 k);
-    // at w = 3 and w = 4 they measure equal to the all-register slabs.
-    static const int tl_env = probe_env("HSFLOW_K2_TL", -1);
-    constexpr int RT = wg_rows_tl(W);
+    // spill).  Used for w = 5 and w = 6 (8 -> 10 rows: 1080p 782 k -> 859 k,
+    // 4K 793 k -> 891 k); at w = 3 and w = 4 they measure equal to the
+    // all-register slabs.
+    constexpr int RT = (W == 5 || W == 6) ? wg_rows_tl(W) : 0;
     if constexpr (RT > 0 && KB * (W - 1) < 8 * RT / 2) {
-        bool on = tl_env < 0 ? (W == 5 || W == 6) : tl_env != 0;
-        if (on && tl_env < 0) {
+        bool on = true;
+        {
             // Taller slabs mean fewer workgroups: keep them only while the
             // launch still fills one round of 2 workgroups per CU (single
             // 1080p pair at w = 5: 323 vs 380 workgroups for 512 slots,
@@ -1188,53 +1055,39 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
 
 template <int W>
 static hipError_t launch_jacobi_w(JacobiArgs a, int KB, hipStream_t s) {
-    if constexpr (W >= 3 && W <= 9) {
-        if (k2_variant() != 0) {
-            switch (KB) {
-            case 1: return launch_jacobi_wgv<W, 1>(a, s);
-            case 2: return launch_jacobi_wgv<W, 2>(a, s);
-            case 3: return launch_jacobi_wgv<W, 3>(a, s);
-            case 4: return launch_jacobi_wgv<W, 4>(a, s);
-            case 5: return launch_jacobi_wgv<W, 5>(a, s);
-            case 6: return launch_jacobi_wgv<W, 6>(a, s);
-            case 8: return launch_jacobi_wgv<W, 8>(a, s);
-            default: return hipErrorInvalidValue;
-            }
+    if constexpr (W >= 3 && W <= 9) {  // K2 workgroup tiles
+        switch (KB) {
+        case 1: return launch_jacobi_wgv<W, 1>(a, s);
+        case 2: return launch_jacobi_wgv<W, 2>(a, s);
+        case 3: return launch_jacobi_wgv<W, 3>(a, s);
+        case 4: return launch_jacobi_wgv<W, 4>(a, s);
+        case 5: return launch_jacobi_wgv<W, 5>(a, s);
+        case 6: return launch_jacobi_wgv<W, 6>(a, s);
+        case 8: return launch_jacobi_wgv<W, 8>(a, s);
+        default: return hipErrorInvalidValue;
         }
+    } else {  // windows 1, 2: per-wave regions
+        switch (KB) {
+        case 1: return launch_jacobi_t<W, 1>(a, s);
+        case 2:
+            if constexpr (kb_ok_packed(W, 2)) return launch_jacobi_t<W, 2>(a, s);
+            break;
+        case 4:
+            if constexpr (kb_ok_packed(W, 4)) return launch_jacobi_t<W, 4>(a, s);
+            break;
+        case 8:
+            if constexpr (kb_ok_packed(W, 8)) return launch_jacobi_t<W, 8>(a, s);
+            break;
+        default: break;
+        }
+        return hipErrorInvalidValue;
     }
-    switch (KB) {
-    case 1: return launch_jacobi_t<W, 1>(a, s);
-    case 2:
-        if constexpr (kb_ok_packed(W, 2)) return launch_jacobi_t<W, 2>(a, s);
-        break;
-    case 4:
-        if constexpr (kb_ok_packed(W, 4)) return launch_jacobi_t<W, 4>(a, s);
-        break;
-    case 8:
-        if constexpr (kb_ok_packed(W, 8)) return launch_jacobi_t<W, 8>(a, s);
-        break;
-    default: break;
-    }
-    return hipErrorInvalidValue;
 }
 
 // One Jacobi pass of a.iters (<= KB) iterations.  Pairs flagged by K1 as
 // non-integral take the f32-gradient path inside the same launch; the caller
 // must then pick KB with kb_supported(W, KB, true).
 hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s) {
-#ifdef HSFLOW_DEV_W  // kernel development builds: one window (and KB) only
-    if (W != HSFLOW_DEV_W) return hipErrorInvalidValue;
-#ifdef HSFLOW_DEV_KB
-    if (KB != HSFLOW_DEV_KB) return hipErrorInvalidValue;
-#ifdef HSFLOW_DEV_NW  // development: other workgroup geometries
-    return launch_jacobi_wg<HSFLOW_DEV_W, HSFLOW_DEV_KB, HSFLOW_DEV_RW, HSFLOW_DEV_NW, 16>(a, s);
-#else
-    return launch_jacobi_wgv<HSFLOW_DEV_W, HSFLOW_DEV_KB>(a, s);
-#endif
-#else
-    return launch_jacobi_w<HSFLOW_DEV_W>(a, KB, s);
-#endif
-#else
     switch (W) {
     case 1: return launch_jacobi_w<1>(a, KB, s);
     case 2: return launch_jacobi_w<2>(a, KB, s);
@@ -1252,7 +1105,6 @@ hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s) {
         return hipGetLastError();
     }
     }
-#endif
 }
 
 }  // namespace hsflow

@@ -1,0 +1,501 @@
+// hsflow_strips.hip -- K4, the streaming Jacobi pass (hornSchunck.cpp:56-74).
+//
+// One wavefront owns a 128-column strip of one pair (lane l: columns 2l and
+// 2l+1 of the strip, as in K2) and a segment of N output rows of it.  It
+// streams the strip's rows top to bottom once per pass and runs the pass's
+// KB Jacobi iterations as KB time-skewed stages in registers:
+//
+//   time step t: row t of the input state (u, v) and its packed gradients
+//     arrive (loaded D steps earlier);  stage 1 updates row t - AR to
+//     iteration 1 (its window rows t - W + 1 .. t are complete), stage 2
+//     updates row t - 2 AR to iteration 2 from stage 1's rows, ...,
+//     stage KB writes row t - KB AR of iteration KB.
+//
+// Each stage keeps only the vertical-sum state of its input rows (4 packed
+// values per field for w = 5, 3 for w = 3); the per-pixel operator
+// (X, Y, T, set up once per row) is kept for the KB AR rows the stages are
+// apart.  So a pass moves each row of u, v and the gradients through HBM
+// once, with no vertical temporal halo inside a segment (only its first
+// KB (W - 1) rows are recomputed by the neighbouring segment), no LDS, no
+// barriers and no load phase: every wave is independent and its loads run
+// D rows ahead of its arithmetic.  Horizontally the strip has K2's halo
+// (KB A columns on the left, KB AR on the right, rounded up to even).
+//
+// The per-pixel operation sequence is K2's (hsflow_kernels.hip): the same
+// horizontal sums (hsum_c2, association by column parity), the same
+// vertical sums by image-row parity (w = 5: pair sums Q at odd rows, cores
+// M at even rows; w = 3: Q at even rows) and the same normalised update
+// (op_setup / op_update), so K4 and K2 give identical bits for every pass,
+// and a solve may mix them (K2 runs the passes K4 does not cover).
+//
+// Outside the image u = v = 0 (BORDER_CONSTANT, hornSchunck.cpp:60-61):
+// columns through the window-mean factor (0 outside, as in K2's border
+// body), rows by a wave-uniform select.  Rows of a stage that precede its
+// first complete window (the segment's start-up) are finite garbage that
+// only ever reaches rows the segment does not store.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "hsflow_internal.h"
+#include "hsflow_device.h"
+
+namespace hsflow {
+
+namespace {
+
+constexpr int kOOB = 0x7FFFFFF0;
+
+// ---- vertical sums, streamed (one field; f2v = the lane's column pair) ----
+// K2's association (by image-row parity), w = 5: Q(t) = h(t) + h(t+1) at
+// odd t; M(y) = Q(y-1) + Q(y+1) at even y; S(y) = h(y-2) + M(y) for even y,
+// M(y-1) + h(y+2) for odd y.  w = 3: Q(t) = h(t) + h(t+1) at even t;
+// S(y) = h(y-1) + Q(y) for even y, Q(y-1) + h(y+1) for odd y.
+// A pass streams its rows downwards (the arrival of h(t) completes the
+// window of y = t - AR) or upwards (completes y = t + A); the same sums
+// come out in either order, so both give K2's bits.
+//
+// w = 5, downwards.  State before an even arrival t: e0 = h(t-4),
+// e1 = h(t-2), q = Q(t-3), x = h(t-1); before an odd arrival: x = M(t-3).
+// w = 5, upwards.  State before an odd arrival t: e0 = h(t+4),
+// e1 = h(t+2), q = Q(t+2), x = h(t+1); before an even arrival: x = M(t+2).
+struct VS5 {
+    f2v e0, e1, q, x;
+};
+template <bool UP, int PT>  // PT: parity of the arriving image row t
+__device__ __forceinline__ f2v vs_arrive(VS5 &s, f2v h) {
+    if constexpr (!UP && PT == 0) {
+        const f2v qn = s.x + h;  // Q(t-1) = h(t-1) + h(t)
+        const f2v m = s.q + qn;  // M(t-2) = Q(t-3) + Q(t-1)
+        const f2v S = s.e0 + m;  // S(t-2) = h(t-4) + M(t-2)
+        s.e0 = s.e1;
+        s.e1 = h;
+        s.q = qn;
+        s.x = m;
+        return S;
+    } else if constexpr (!UP) {
+        const f2v S = s.x + h;  // S(t-2) = M(t-3) + h(t)
+        s.x = h;
+        return S;
+    } else if constexpr (PT == 1) {
+        const f2v qn = h + s.x;  // Q(t) = h(t) + h(t+1)
+        const f2v m = qn + s.q;  // M(t+1) = Q(t) + Q(t+2)
+        const f2v S = m + s.e0;  // S(t+2) = M(t+1) + h(t+4)
+        s.e0 = s.e1;
+        s.e1 = h;
+        s.q = qn;
+        s.x = m;
+        return S;
+    } else {
+        const f2v S = h + s.x;  // S(t+2) = h(t) + M(t+2)
+        s.x = h;
+        return S;
+    }
+}
+// w = 3, downwards.  State before an odd arrival t: h1 = h(t-1),
+// h2 = h(t-2); before an even arrival: q = Q(t-2).
+// w = 3, upwards.  State before an even arrival t: h1 = h(t+1),
+// h2 = h(t+2); before an odd arrival: q = Q(t+1).
+struct VS3 {
+    f2v h1, h2, q;
+};
+template <bool UP, int PT>
+__device__ __forceinline__ f2v vs_arrive(VS3 &s, f2v h) {
+    if constexpr (!UP && PT == 1) {
+        const f2v qn = s.h1 + h;  // Q(t-1) = h(t-1) + h(t)
+        const f2v S = s.h2 + qn;  // S(t-1) = h(t-2) + Q(t-1)
+        s.q = qn;
+        s.h2 = h;
+        return S;
+    } else if constexpr (!UP) {
+        const f2v S = s.q + h;  // S(t-1) = Q(t-2) + h(t)
+        s.h1 = h;
+        return S;
+    } else if constexpr (PT == 0) {
+        const f2v qn = h + s.h1;  // Q(t) = h(t) + h(t+1)
+        const f2v S = qn + s.h2;  // S(t+1) = Q(t) + h(t+2)
+        s.q = qn;
+        s.h2 = h;
+        return S;
+    } else {
+        const f2v S = h + s.q;  // S(t+1) = h(t) + Q(t+1)
+        s.h1 = h;
+        return S;
+    }
+}
+
+template <int W> struct VSOf;
+template <> struct VSOf<3> { using type = VS3; };
+template <> struct VSOf<5> { using type = VS5; };
+
+template <bool G32> struct RowIn;
+template <> struct RowIn<false> {  // packed exact integer gradients
+    f2v u, v;
+    u2v g;
+};
+template <> struct RowIn<true> {  // f32 gradient planes (non-integral inputs)
+    f2v u, v, gx, gy, gt;
+};
+
+struct Rsrc {
+    __amdgpu_buffer_rsrc_t u, v, g, gx, gy, gt, uo, vo;
+};
+
+template <bool X2>
+__device__ __forceinline__ f2v ld2(__amdgpu_buffer_rsrc_t r, int vo_e, int vo_o, int so) {
+    if constexpr (X2) {
+        const u2v a = __builtin_amdgcn_raw_buffer_load_b64(r, vo_e, so, 0);
+        return f2v{__uint_as_float(a.x), __uint_as_float(a.y)};
+    } else {
+        return f2v{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo_e, so, 0)),
+                   __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo_o, so, 0))};
+    }
+}
+
+template <bool X2, bool G32>
+__device__ __forceinline__ void load_row(RowIn<G32> &d, const Rsrc &rs, int vo_e, int vo_o,
+                                         int so) {
+    d.u = ld2<X2>(rs.u, vo_e, vo_o, so);
+    d.v = ld2<X2>(rs.v, vo_e, vo_o, so);
+    if constexpr (G32) {
+        d.gx = ld2<X2>(rs.gx, vo_e, vo_o, so);
+        d.gy = ld2<X2>(rs.gy, vo_e, vo_o, so);
+        d.gt = ld2<X2>(rs.gt, vo_e, vo_o, so);
+    } else if constexpr (X2) {
+        d.g = __builtin_amdgcn_raw_buffer_load_b64(rs.g, vo_e, so, 0);
+    } else {
+        d.g = u2v{__builtin_amdgcn_raw_buffer_load_b32(rs.g, vo_e, so, 0),
+                  __builtin_amdgcn_raw_buffer_load_b32(rs.g, vo_o, so, 0)};
+    }
+}
+
+template <bool G32>
+__device__ __forceinline__ void row_op(float alpha2, const RowIn<G32> &d, f2v &X, f2v &Y,
+                                       f2v &T) {
+    float ixe, iye, ite, ixo, iyo, ito;
+    if constexpr (G32) {
+        ixe = d.gx.x; ixo = d.gx.y;
+        iye = d.gy.x; iyo = d.gy.y;
+        ite = d.gt.x; ito = d.gt.y;
+    } else {
+        unpack_grad(d.g.x, ixe, iye, ite);
+        unpack_grad(d.g.y, ixo, iyo, ito);
+    }
+    op_setup(alpha2, ixe, iye, ite, ixo, iyo, ito, X, Y, T);
+}
+
+template <int W>
+__device__ __forceinline__ void hrow(f2v u, f2v v, f2v &hu, f2v &hv) {
+    float a, b, c, d;
+    hsum_c2<W>(u.x, u.y, v.x, v.y, a, b, c, d);
+    hu = f2v{a, b};
+    hv = f2v{c, d};
+}
+
+}  // namespace
+
+// Segment body: rows [a, b) of strip columns [c0, c0 + 128) of one pair,
+// streamed downwards or (UP) upwards.  U = unroll period (multiple of the
+// operator ring KB*AR, of 2 and of D).
+template <int W, int KB, int D, int U, bool X2, bool G32, bool UP>
+__device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, int plane_bytes,
+                                           int c0, int a, int b) {
+    constexpr int A = W - W / 2 - 1, AR = W / 2;
+    static_assert(A == AR, "K4 is built for odd windows");
+    constexpr int L = KB * AR;  // operator ring: the rows t -+ AR .. t -+ KB AR
+    static_assert(U % L == 0 && U % 2 == 0 && U % D == 0, "unroll period");
+    using VS = typename VSOf<W>::type;
+    constexpr int HLc = KB * A + ((KB * A) & 1), HRc = KB * AR + ((KB * AR) & 1);
+    const int lane = threadIdx.x & 63;
+    const int cols = p.cols, rows = p.rows;
+    const int gce = c0 + 2 * lane;  // this lane's even image column
+    const bool ce = (unsigned)gce < (unsigned)cols;
+    const bool co = (unsigned)(gce + 1) < (unsigned)cols;
+    // window-mean factor of this lane's columns: 1/w^2 inside the image, 0
+    // outside (there the loaded gradients are 0 too, so the update is 0)
+    const f2v colm = {ce ? p.inv_w2 : 0.f, co ? p.inv_w2 : 0.f};
+    const int c4 = gce * 4;
+    // per-lane load offsets (the row goes in soffset); X2: one 8-byte word
+    // per column pair, wholly inside or outside the image (even width)
+    const int ld_e = ce ? c4 : kOOB;
+    const int ld_o = co ? c4 + 4 : kOOB;
+    const bool st_lane = lane >= HLc / 2 && lane < (128 - HRc) / 2;
+    const int st_e = (st_lane && ce) ? c4 : kOOB;
+    const int st_o = (st_lane && co) ? c4 + 4 : kOOB;
+
+    Rsrc rs;
+    rs.u = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_in ? p.u_in + pbase : p.u_out + pbase),
+                                             0, p.u_in ? plane_bytes : 0, 0x00020000);
+    rs.v = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_in ? p.v_in + pbase : p.v_out + pbase),
+                                             0, p.v_in ? plane_bytes : 0, 0x00020000);
+    rs.g = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gpack + pbase), 0,
+                                             G32 ? 0 : plane_bytes, 0x00020000);
+    rs.gx = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gx + pbase), 0, G32 ? plane_bytes : 0,
+                                              0x00020000);
+    rs.gy = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gy + pbase), 0, G32 ? plane_bytes : 0,
+                                              0x00020000);
+    rs.gt = __builtin_amdgcn_make_buffer_rsrc((void *)(p.gt + pbase), 0, G32 ? plane_bytes : 0,
+                                              0x00020000);
+    rs.uo = __builtin_amdgcn_make_buffer_rsrc((void *)(p.u_out + pbase), 0, plane_bytes,
+                                              0x00020000);
+    rs.vo = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0, plane_bytes,
+                                              0x00020000);
+
+    const float alpha2 = p.alpha2;
+    // first and last input row of the stream; the first is even (segment
+    // starts are even, and so is KB A; an upward stream starts one row
+    // lower when needed: a real row below only widens the complete part of
+    // its windows)
+    const int t_first = UP ? ((b - 1 + KB * AR) + 1) & ~1 : a - KB * A;
+    const int t_last = UP ? a - KB * A : b - 1 + KB * AR;
+    constexpr int dir = UP ? -1 : 1;
+    auto issue = [&](RowIn<G32> &d, int r) {
+        const bool rin = (unsigned)r < (unsigned)rows;
+        const int so = rin ? r * cols * 4 : 0;
+        load_row<X2, G32>(d, rs, rin ? launder(ld_e) : kOOB, rin ? launder(ld_o) : kOOB, so);
+    };
+
+    RowIn<G32> buf[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) issue(buf[k], t_first + dir * k);
+
+    const f2v z = {0.f, 0.f};
+    f2v OX[L], OY[L], OT[L];
+#pragma unroll
+    for (int k = 0; k < L; ++k) OX[k] = OY[k] = OT[k] = z;
+    VS su[KB], sv[KB];
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+        if constexpr (W == 5) {
+            su[j] = VS{z, z, z, z};
+            sv[j] = VS{z, z, z, z};
+        } else {
+            su[j] = VS{z, z, z};
+            sv[j] = VS{z, z, z};
+        }
+    }
+
+    // one unrolled block of U time steps from row tb (even); ROWE: some
+    // stage row of the block may lie outside the image (top / bottom
+    // segments)
+    auto block = [&](int tb, auto rowe_c) {
+        constexpr bool ROWE = decltype(rowe_c)::value;
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int t = tb + dir * k;
+            // 1. this row's input (loaded D steps ago), then the load of
+            //    row t + D (t - D upwards) into the freed slot
+            const RowIn<G32> cur = buf[k % D];
+            issue(buf[k % D], t + dir * D);
+            // 2. level-0 horizontal sums of row t
+            f2v hu, hv;
+            hrow<W>(cur.u, cur.v, hu, hv);
+            // 3. the stages: stage j (1-based) receives row t -+ (j-1) AR of
+            //    iteration j-1 and updates row t -+ j AR to iteration j
+#pragma unroll
+            for (int j = 0; j < KB; ++j) {
+                const int y = t - dir * (j + 1) * AR;
+                // image-row parity of the arriving row t -+ j AR (tb even)
+                const int pt = (k + j * AR) & 1;
+                f2v Su, Sv;
+                if (pt == 0) {
+                    Su = vs_arrive<UP, 0>(su[j], hu);
+                    Sv = vs_arrive<UP, 0>(sv[j], hv);
+                } else {
+                    Su = vs_arrive<UP, 1>(su[j], hu);
+                    Sv = vs_arrive<UP, 1>(sv[j], hv);
+                }
+                const int sl = ((k - (j + 1) * AR) % L + L) % L;  // operator slot of row y
+                f2v nu, nv;
+                op_update(Su, Sv, colm, OX[sl], OY[sl], OT[sl], nu, nv);
+                if constexpr (ROWE) {
+                    if ((unsigned)y >= (unsigned)rows) {  // rows outside the image: 0
+                        nu = z;
+                        nv = z;
+                    }
+                }
+                if (j + 1 < KB) {
+                    hrow<W>(nu, nv, hu, hv);
+                } else if (y >= a && y < b) {
+                    const int so = y * cols * 4;
+                    if constexpr (X2) {
+                        __builtin_amdgcn_raw_buffer_store_b64(
+                            u2v{__float_as_uint(nu.x), __float_as_uint(nu.y)}, rs.uo, st_e, so,
+                            2);
+                        __builtin_amdgcn_raw_buffer_store_b64(
+                            u2v{__float_as_uint(nv.x), __float_as_uint(nv.y)}, rs.vo, st_e, so,
+                            2);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.x), rs.uo, st_e,
+                                                              so, 2);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.y), rs.uo, st_o,
+                                                              so, 2);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.x), rs.vo, st_e,
+                                                              so, 2);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.y), rs.vo, st_o,
+                                                              so, 2);
+                    }
+                }
+            }
+            // 4. operator of row t, into the slot stage KB has just read
+            row_op<G32>(alpha2, cur, OX[k % L], OY[k % L], OT[k % L]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    // three loops, so the blocks whose stage rows all lie inside the image
+    // run a body without row zeroing (one body per loop: a two-body loop
+    // makes the allocator spill); the rarely used variants take one loop
+    auto more = [&](int tb) { return UP ? tb >= t_last : tb <= t_last; };
+    // the block's stage rows: downwards [tb - KB AR, tb + U - 1 - AR],
+    // upwards [tb - (U - 1) + A, tb + KB A]
+    auto edge_first = [&](int tb) { return UP ? tb + KB * A >= rows : tb - KB * AR < 0; };
+    auto inside_end = [&](int tb) {
+        return UP ? tb - (U - 1) + A >= 0 : tb + U - 1 - AR < rows;
+    };
+    int tb = t_first;
+    if constexpr (X2 && !G32) {
+        for (; more(tb) && edge_first(tb); tb += dir * U) block(tb, std::true_type{});
+        for (; more(tb) && inside_end(tb); tb += dir * U) block(tb, std::false_type{});
+    }
+    for (; more(tb); tb += dir * U) block(tb, std::true_type{});
+}
+
+template <int W, int KB, int D, int U, bool UP>
+__device__ __forceinline__ void strip_variant(const JacobiArgs &p, size_t pbase,
+                                              int plane_bytes, int c0, int a, int b, bool g32) {
+    if (g32) {
+        if ((p.cols & 1) == 0)
+            strip_body<W, KB, D, U, true, true, UP>(p, pbase, plane_bytes, c0, a, b);
+        else
+            strip_body<W, KB, D, U, false, true, UP>(p, pbase, plane_bytes, c0, a, b);
+    } else {
+        if ((p.cols & 1) == 0)
+            strip_body<W, KB, D, U, true, false, UP>(p, pbase, plane_bytes, c0, a, b);
+        else
+            strip_body<W, KB, D, U, false, false, UP>(p, pbase, plane_bytes, c0, a, b);
+    }
+}
+
+// ---------------------------------------------------------------- kernel
+// One wave per (pair, segment, strip); 64-thread workgroups, 8 per CU (two
+// waves per SIMD: up to 256 VGPRs).  Logical order: pair, segment, strip
+// (strips fastest), so the strips that share halo columns run side by side;
+// the XCD-aware remap gives each XCD a contiguous run of them (its L2
+// serves the shared halo columns and the rows two segments both read).
+template <int W, int KB, int D, int U>
+__global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs p) {
+    const int nblk = gridDim.x;
+    const int lin = blockIdx.x;
+    const int qn = nblk >> 3, rem = nblk & 7, xcd = lin & 7;
+    const int logical = xcd * qn + min(xcd, rem) + (lin >> 3);
+    const int nstrips = p.tiles_x, nseg = p.tiles_y;
+    const int per_pair = nstrips * nseg;
+    const int pair = logical / per_pair;
+    if (pair >= p.batch) return;
+    const int r = logical - pair * per_pair;
+    const int seg = r / nstrips, sx = r - seg * nstrips;
+    constexpr int A = W - W / 2 - 1, AR = W / 2;
+    constexpr int HLc = KB * A + ((KB * A) & 1), HRc = KB * AR + ((KB * AR) & 1);
+    constexpr int OX = 128 - HLc - HRc;
+    const int c0 = sx * OX - HLc;
+    const int a = seg * p.seg_rows;
+    const int b = min(p.rows, a + p.seg_rows);  // segments end inside the image
+    const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)p.cols;
+    const int plane_bytes = p.rows * p.cols * 4;
+    const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
+    // successive passes stream in opposite directions: the rows a pass
+    // wrote last are the first the next one reads, while they may still be
+    // in the Infinity Cache
+    if (p.strip_up)
+        strip_variant<W, KB, D, U, true>(p, pbase, plane_bytes, c0, a, b, g32);
+    else
+        strip_variant<W, KB, D, U, false>(p, pbase, plane_bytes, c0, a, b, g32);
+}
+
+// ------------------------------------------------------------- launcher
+namespace {
+template <int W, int KB> struct StripCfg;
+template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };
+template <> struct StripCfg<3, 8> { static constexpr int D = 2, U = 8; };
+}  // namespace
+
+bool strip_supported(int W, int KB) { return (W == 5 && KB == 6) || (W == 3 && KB == 8); }
+
+// Segment rows for a launch.  Each wave streams N rows plus the KB (W - 1)
+// halo rows its stages need, so tall segments waste little work and few
+// re-read rows, while short ones give more waves.  Policy (measured, DESIGN.md
+// §4 K4): the shortest segment of at least 72 rows -- with N + KB (W - 1)
+// a multiple of the unroll period -- whose waves fit one round of the
+// chip's slots (two waves per SIMD); if even the tallest sensible one (240
+// rows) needs several rounds, the height with the fewest rounds x steps.
+// `override_rows` > 0 forces N (rounded up to the period).
+int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int *nseg_out,
+                   int *nstrips_out, int override_rows) {
+    const int A = W - W / 2 - 1, AR = W / 2;
+    const int HLc = KB * A + ((KB * A) & 1), HRc = KB * AR + ((KB * AR) & 1);
+    const int ox = 128 - HLc - HRc;
+    const int U = (W == 5) ? 12 : 8;
+    const int nstrips = (cols + ox - 1) / ox;
+    const long strips = (long)nstrips * batch;
+    const int halo = KB * (W - 1);
+    auto aligned = [&](int n) {  // smallest n' >= n with (n' + halo) % U == 0, n' even
+        while ((n + halo) % U != 0 || (n & 1)) ++n;
+        return n;
+    };
+    auto waves = [&](int n) { return strips * ((rows + n - 1) / n); };
+    int best_n = aligned(override_rows > 0 ? override_rows : 72);
+    if (override_rows <= 0 && waves(best_n) > slots) {
+        long best = -1;
+        for (int n = best_n; n <= 240; n = aligned(n + 1)) {
+            const long w = waves(n);
+            if (w <= slots) {
+                best_n = n;
+                break;
+            }
+            const long t = (w + slots - 1) / slots * (n + halo);
+            if (best < 0 || t < best) {
+                best = t;
+                best_n = n;
+            }
+        }
+    }
+    *nseg_out = (rows + best_n - 1) / best_n;
+    *nstrips_out = nstrips;
+    return best_n;
+}
+
+// K4 pays when its waves, at the policy's segment height, fill a good part
+// of the chip (a single 1080p pair has 19 strips: ~285 waves for 2048
+// slots, and K2's tiles run it faster; a 4K pair's 37 strips fill 0.54).
+bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
+    int nseg = 0, nstrips = 0;
+    strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 0);
+    return (long)nseg * nstrips * batch * 20 >= (long)slots * 7;  // >= 0.35 of the slots
+}
+
+// One K4 pass of `a.batch` pairs in segments of `seg_rows` rows (the
+// caller's choice: strip_seg_rows over every pair in flight).
+hipError_t launch_jacobi_strip(JacobiArgs a, int W, int KB, int seg_rows, hipStream_t s) {
+    int nseg = 0, nstrips = 0;
+    a.seg_rows = strip_seg_rows(W, KB, a.rows, a.cols, a.batch, 1, &nseg, &nstrips,
+                                seg_rows > 0 ? seg_rows : 84);
+    a.tiles_x = nstrips;
+    a.tiles_y = nseg;
+    const long waves = (long)nstrips * nseg * a.batch;
+    if (waves <= 0 || waves > 0x7FFFFFFFL) return hipErrorInvalidValue;
+    dim3 grd((unsigned)waves, 1, 1);
+    if (W == 5 && KB == 6) {
+        using C = StripCfg<5, 6>;
+        hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U>), grd, dim3(64), 0, s, a);
+    } else if (W == 3 && KB == 8) {
+        using C = StripCfg<3, 8>;
+        hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U>), grd, dim3(64), 0, s, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace hsflow

@@ -66,9 +66,10 @@ typedef struct hsflow_ctx hsflow_ctx;
 int hsflow_version(void);
 const char *hsflow_status_string(int status);
 
-/* Build flags of the loaded library.  HSFLOW_BUILD_PROBE: the diagnostic
- * build (`make probe`, libhsflow_probe.so) whose kernels honour HSFLOW_*
- * environment switches; the product library ignores the environment. */
+/* Build flags of the loaded library.  0 for every build today: the
+ * environment-honouring diagnostic ("probe") build of v2.0 is retired, and
+ * the library reads no environment variable.  HSFLOW_BUILD_PROBE stays
+ * defined so callers that test for it keep compiling. */
 #define HSFLOW_BUILD_PROBE 1
 int hsflow_build_flags(void);
 
@@ -143,11 +144,25 @@ int hsflow_jacobi_device(int rows, int cols, int batch, int window, int iters,
 int hsflow_set_iters_per_launch(int k);
 int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
 
-/* Kernel of the Jacobi passes: 0 = automatic (default), 2 = K2 register
- * tiles, one launch per pass of iters_per_launch iterations.  Every choice
- * gives identical bits.  Process-wide; not thread-safe against running
- * solves. */
+/* Kernel of the Jacobi passes (one launch per pass of iters_per_launch
+ * iterations): 0 = automatic (default: K4 streaming strips where built --
+ * windowSize 3 and 5 at their default depth -- K2 register tiles
+ * elsewhere), 2 = K2 everywhere, 4 = K4 where built.  Every choice gives
+ * identical bits.  Process-wide; not thread-safe against running solves. */
 int hsflow_set_jacobi_kernel(int k);
+
+/* K4 streaming passes: `seg_rows` = rows per segment (each wave streams
+ * one segment of one 128-column strip), 0 = automatic (default);
+ * `alternate` = 1 (default): successive passes stream in opposite
+ * directions, 0: every pass top to bottom.  Results are bit-identical for
+ * every choice.  Process-wide; not thread-safe against running solves. */
+int hsflow_set_strip_options(int seg_rows, int alternate);
+
+/* Name of the kernel that runs the full-depth Jacobi passes of a solve of
+ * this shape under the current settings ("hs_jacobi_strip_kernel",
+ * "hs_jacobi_wg_kernel", "hs_jacobi_kernel" or "hs_jacobi_generic_kernel");
+ * a static string.  For profiles and the bench's roofline record. */
+const char *hsflow_jacobi_kernel_name(int rows, int cols, int batch, int window);
 
 /* Batches of >= 2 pairs are split over up to n side streams (forked from and
  * joined back to the caller's stream with events) so that concurrent Jacobi

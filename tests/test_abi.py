@@ -43,13 +43,23 @@ def test_workspace_bytes():
 
 
 def test_iters_per_launch_policy():
-    # measured defaults: w 5 runs 6 iterations per pass when a
-    # launch has rounds of workgroups, 8 when one round does not fill the chip
+    # measured defaults: K4 streams w 5 at 6 and w 3 at 8
+    # iterations per pass where its waves fill the chip; launches too small
+    # for it run K2, at 6 (w 5) when a launch has rounds of workgroups and
+    # 8 when one round does not fill the chip
     assert hsflow.iters_per_launch(1080, 1920, 8, 5) == 6
     assert hsflow.iters_per_launch(2160, 3840, 1, 5) == 6
+    assert hsflow.jacobi_kernel_name(2160, 3840, 1, 5) == "hs_jacobi_strip_kernel"
     assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 8
-    assert hsflow.iters_per_launch(375, 1242, 1, 5) == 8
+    assert hsflow.jacobi_kernel_name(1080, 1920, 1, 5) == "hs_jacobi_wg_kernel"
     assert hsflow.iters_per_launch(1080, 1920, 1, 3) == 8
+    try:
+        hsflow.set_jacobi_kernel(2)
+        assert hsflow.iters_per_launch(1080, 1920, 8, 5) == 6
+        assert hsflow.iters_per_launch(1080, 1920, 1, 5) == 8
+        assert hsflow.iters_per_launch(375, 1242, 1, 5) == 8
+    finally:
+        hsflow.set_jacobi_kernel(0)
     assert hsflow.iters_per_launch(1080, 1920, 1, 12) == 1
     with pytest.raises(hsflow.HsflowError):
         hsflow.set_iters_per_launch(-1)
@@ -61,12 +71,35 @@ def test_iters_per_launch_policy():
 
 
 def test_jacobi_kernel_selector():
-    """0 = automatic, 2 = K2 tiles one launch per pass; others rejected."""
-    for bad in (-1, 1, 3, 99):
+    """0 = automatic (K4 strips where built), 2 = K2 tiles, 4 = K4 where
+    built; others rejected.  The kernel name follows the choice (no GPU
+    call: the name comes from the launcher's own selection logic)."""
+    for bad in (-1, 1, 3, 5, 99):
         with pytest.raises(hsflow.HsflowError):
             hsflow.set_jacobi_kernel(bad)
-    for k in (2, 0):
-        hsflow.set_jacobi_kernel(k)
+    try:
+        hsflow.set_jacobi_kernel(2)
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 5) == "hs_jacobi_wg_kernel"
+        hsflow.set_jacobi_kernel(4)
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 5) == "hs_jacobi_strip_kernel"
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 3) == "hs_jacobi_strip_kernel"
+        # K4 is built for windows 3 and 5 at their default depth only
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 7) == "hs_jacobi_wg_kernel"
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 2) == "hs_jacobi_kernel"
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 15) == "hs_jacobi_generic_kernel"
+        hsflow.set_iters_per_launch(4)  # a depth K4 is not built for: K2
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 5) == "hs_jacobi_wg_kernel"
+    finally:
+        hsflow.set_iters_per_launch(0)
+        hsflow.set_jacobi_kernel(0)
+    assert hsflow.jacobi_kernel_name(2160, 3840, 2, 5) == "hs_jacobi_strip_kernel"
+    assert hsflow.jacobi_kernel_name(0, 10, 1, 5) == ""
+    with pytest.raises(hsflow.HsflowError):
+        hsflow.set_strip_options(-1)
+    with pytest.raises(hsflow.HsflowError):
+        hsflow.lib().hsflow_set_strip_options(0, 2) and hsflow._check(-1)
+    hsflow.set_strip_options(48, False)
+    hsflow.set_strip_options(0, True)
 
 
 def test_device_entry_points_validate_before_touching_the_gpu():

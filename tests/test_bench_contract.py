@@ -41,7 +41,12 @@ def test_bench_prints_one_contract_line():
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    # a physical fraction: the algorithmic bytes of one blocked pass
+    assert 0 < r["frac"] <= 1.0
+    assert r["kernel"] in ("hs_jacobi_strip_kernel", "hs_jacobi_wg_kernel")
     assert "workload" in d["config"]
+    # the timed output was checked after NaN-filling it before the steps
+    assert d["parity"]["outputs_nan_filled_before_timing"] is True
 
 
 def test_bench_refuses_diagnostic_environment():
@@ -95,3 +100,42 @@ def test_bench_golden_fixture_covers_the_bench_workloads():
         assert np.isfinite(us).all() and float(np.abs(us).max()) <= e["max_u"] * (1 + 1e-6)
         # SURVEY §8d sanity: mean u ~ dx / 8 (Sobel scaling) for dx = +1.5 px
         assert 0.05 < e["sum_u"] / (w["rows"] * w["cols"]) < 0.3
+
+
+def test_gpus_flag_is_authoritative_world_selection():
+    """--gpus N decides the rank count (bench.world_from_env): no launcher
+    and N > 1 -> bench.py starts N ranks itself; a launcher whose
+    WORLD_SIZE disagrees -> refuse; never a silent one-GPU line."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.world_from_env(1, {}) == ("run", 1)
+    assert bench.world_from_env(2, {}) == ("launch", 2)
+    assert bench.world_from_env(8, {}) == ("launch", 8)
+    assert bench.world_from_env(2, {"WORLD_SIZE": "2"}) == ("run", 2)
+    assert bench.world_from_env(8, {"WORLD_SIZE": "1"}) == ("refuse", 1)
+    assert bench.world_from_env(1, {"WORLD_SIZE": "4"}) == ("refuse", 4)
+
+
+def test_gpus_2_without_a_launcher_starts_two_ranks():
+    """`python bench.py --gpus 2 --launch-check` (no WORLD_SIZE) launches two
+    rank processes through torch.distributed.run on 127.0.0.1; rank 0 prints
+    n_gpus 2 after a gloo all-reduce that sees both ranks (the plumbing the
+    driver's 8-GPU run relies on; no GPU work)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--launch-check"], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2
+    assert lines[0]["launcher"] == "torch.distributed.run"
+
+
+def test_gpus_mismatch_with_launcher_refuses():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2 and "WORLD_SIZE=1" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]

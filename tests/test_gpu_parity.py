@@ -383,7 +383,7 @@ def test_cpp_main_driver_reproduces_reference_plot(tmp_path, tag):
     assert norm_rel_err(u, uo) <= TOL
 
 
-@pytest.mark.parametrize("kernel", [0, 2])  # automatic, K2 launch per pass
+@pytest.mark.parametrize("kernel", [0, 2, 4])  # automatic, K2 tiles, K4 strips
 @pytest.mark.parametrize("batch", [1, 3])
 def test_device_solve_captures_into_a_hip_graph(hs, batch, kernel):
     """include/hsflow.h: the *_device calls are stream-ordered and never
