@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -148,11 +149,13 @@ int elem_size(int dtype) {
     }
 }
 
-// element size of the device copy of a host input (F64 is narrowed to f32)
-int dev_elem_size(int dtype) { return dtype == HSFLOW_F64 ? 4 : elem_size(dtype); }
+// element size of the device copy of a host input (every input type is
+// uploaded as it is: K1 reads u8, f16, f32 and f64 frames)
+int dev_elem_size(int dtype) { return elem_size(dtype); }
 
 bool device_dtype_ok(int dtype) {
-    return dtype == HSFLOW_U8 || dtype == HSFLOW_F32 || dtype == HSFLOW_F16;
+    return dtype == HSFLOW_U8 || dtype == HSFLOW_F32 || dtype == HSFLOW_F16 ||
+           dtype == HSFLOW_F64;
 }
 
 // `batch`: every pair in flight at once (the whole batch, also when it is
@@ -397,7 +400,7 @@ int gradients_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in
     if (!sizes_ok(rows, cols, batch))
         return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
     if (!device_dtype_ok(dtype_in))
-        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8, F16 or F32");
+        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8, F16, F32 or F64");
     if (!I0 || !I1 || !workspace) return fail(ctx, HSFLOW_ERR_ARG, "null device pointer");
     Workspace w = carve(workspace, rows, cols, batch);
     if (ws_bytes < w.bytes)
@@ -438,30 +441,15 @@ int grow_host(hsflow_ctx *ctx, size_t need) {
     return HSFLOW_OK;
 }
 
-// Host rows (any supported dtype, any step) -> dense device U8 or F32.
-// F64 input (CV_64FC1) is narrowed to f32 on the host first.
+// Host rows (any supported dtype, any step) -> dense device rows of the
+// same type (K1 takes the Sobel sums of CV_64FC1 frames in float64, as
+// hornSchunck.cpp:23-28 do, and rounds each gradient to f32 once).
 int upload(hsflow_ctx *ctx, const void *src, int dtype, int rows, int cols, size_t step,
            void *dst, int *dev_dtype) {
-    if (device_dtype_ok(dtype)) {
-        const size_t es = (size_t)elem_size(dtype);
-        HIP_TRY(ctx, hipMemcpy2DAsync(dst, cols * es, src, step, cols * es, rows,
-                                      hipMemcpyHostToDevice, ctx->stream));
-        *dev_dtype = dtype;
-        return HSFLOW_OK;
-    }
-    // F64: narrow through the pinned stage
-    int rc = grow_host(ctx, (size_t)rows * cols * 4);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // stage may be in use
-    for (int r = 0; r < rows; ++r) {
-        const double *s = (const double *)((const char *)src + (size_t)r * step);
-        float *d = ctx->h_stage + (size_t)r * cols;
-        for (int c = 0; c < cols; ++c) d[c] = (float)s[c];
-    }
-    HIP_TRY(ctx, hipMemcpyAsync(dst, ctx->h_stage, (size_t)rows * cols * 4,
-                                hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    *dev_dtype = HSFLOW_F32;
+    const size_t es = (size_t)elem_size(dtype);
+    HIP_TRY(ctx, hipMemcpy2DAsync(dst, cols * es, src, step, cols * es, rows,
+                                  hipMemcpyHostToDevice, ctx->stream));
+    *dev_dtype = dtype;
     return HSFLOW_OK;
 }
 
@@ -586,7 +574,7 @@ int pyramid_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, 
     if (!sizes_ok(rows, cols, batch))
         return fail(ctx, HSFLOW_ERR_ARG, "bad size %dx%d batch %d", rows, cols, batch);
     if (!device_dtype_ok(dtype_in))
-        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8, F16 or F32");
+        return fail(ctx, HSFLOW_ERR_ARG, "device input dtype must be U8, F16, F32 or F64");
     if (!I0 || !I1 || !u || !v || !ws)
         return fail(ctx, HSFLOW_ERR_ARG, "null device pointer");
     const PyrLayout L = pyr_layout(rows, cols, batch, levels);
@@ -839,24 +827,42 @@ int hsflow_flow_multi(const int *devices, int n_devices, int batch,
         if (devices[k] < 0 || devices[k] >= ndev)
             return fail(nullptr, HSFLOW_ERR_NODEV, "device %d of %d", devices[k], ndev);
     const int nw = std::min(n_devices, batch);
+    // Contexts (device buffers, pinned stage, stream) are kept across calls,
+    // one per (device, slot): a caller that sends frame after frame through
+    // here pays no allocation or device synchronisation per call.  One
+    // multi call at a time owns them.
+    static std::mutex mu;
+    static std::vector<std::vector<hsflow_ctx *>> ctx_pool;  // [device][slot]
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)ctx_pool.size() < ndev) ctx_pool.resize(ndev);
+    std::vector<hsflow_ctx **> slot(nw);
+    for (int k = 0; k < nw; ++k) {
+        int dup = 0;  // earlier workers on the same device
+        for (int i = 0; i < k; ++i) dup += devices[i] == devices[k];
+        auto &dv = ctx_pool[devices[k]];
+        if ((int)dv.size() <= dup) dv.resize(dup + 1, nullptr);
+        slot[k] = &dv[dup];
+    }
     std::vector<int> rc(nw, HSFLOW_OK);
     std::vector<std::string> msg(nw);
     std::vector<std::thread> pool;
     pool.reserve(nw);
     for (int k = 0; k < nw; ++k) {
         pool.emplace_back([&, k] {
-            hsflow_ctx *ctx = nullptr;
-            int r = hsflow_create(&ctx, devices[k]);
-            if (r) {
-                rc[k] = r;
-                msg[k] = hsflow_last_error(nullptr);  // this worker's message
-                return;
+            int r = HSFLOW_OK;
+            if (!*slot[k]) {
+                r = hsflow_create(slot[k], devices[k]);
+                if (r) {
+                    rc[k] = r;
+                    msg[k] = hsflow_last_error(nullptr);  // this worker's message
+                    return;
+                }
             }
+            hsflow_ctx *ctx = *slot[k];
             for (int j = k; j < batch && r == HSFLOW_OK; j += nw)
                 r = hsflow_flow(ctx, I0[j], I1[j], dtype_in, rows, cols, in_step0, in_step1,
                                 window, iters, alpha, u[j], v[j], dtype_out, out_step);
             if (r) msg[k] = hsflow_last_error(ctx);
-            hsflow_destroy(ctx);
             rc[k] = r;
         });
     }

@@ -45,9 +45,11 @@ __device__ __forceinline__ int reflect101(int p, int len) {
     return p >= len ? 2 * (len - 1) - p : p;
 }
 
-template <typename T> __device__ __forceinline__ float ld_px(const T *p) {
-    return (float)*p;
-}
+// K1 arithmetic type: double for CV_64FC1 frames (hornSchunck.cpp:23-28 take
+// the Sobel sums in float64; each gradient is rounded to f32 once), float
+// otherwise (exact for 8-bit-valued frames either way)
+template <typename T> struct GradMath { using type = float; };
+template <> struct GradMath<double> { using type = double; };
 
 // ----------------------------------------------------------------------- K1
 // block 64 x 4, one pixel per thread; grid (ceil(cols/64), ceil(rows/4), batch)
@@ -56,6 +58,7 @@ __global__ __launch_bounds__(256) void hs_gradients_kernel(
     const T *__restrict__ I0, const T *__restrict__ I1, int rows, int cols,
     uint32_t *__restrict__ gpack, float *__restrict__ gx, float *__restrict__ gy,
     float *__restrict__ gt, uint32_t *__restrict__ flags) {
+    using F = typename GradMath<T>::type;
     const int c = blockIdx.x * 64 + threadIdx.x;
     const int r = blockIdx.y * 4 + threadIdx.y;
     const size_t plane = (size_t)rows * cols;
@@ -67,21 +70,21 @@ __global__ __launch_bounds__(256) void hs_gradients_kernel(
         const int cm = reflect101(c - 1, cols), cp = reflect101(c + 1, cols);
         const T *pm = a + (size_t)rm * cols, *p0 = a + (size_t)r * cols,
                 *pp = a + (size_t)rp * cols;
-        const float m_m = ld_px(pm + cm), m_0 = ld_px(pm + c), m_p = ld_px(pm + cp);
-        const float z_m = ld_px(p0 + cm), z_0 = ld_px(p0 + c), z_p = ld_px(p0 + cp);
-        const float p_m = ld_px(pp + cm), p_0 = ld_px(pp + c), p_p = ld_px(pp + cp);
-        const float nxt = ld_px(b + (size_t)r * cols + c);
+        const F m_m = (F)pm[cm], m_0 = (F)pm[c], m_p = (F)pm[cp];
+        const F z_m = (F)p0[cm], z_0 = (F)p0[c], z_p = (F)p0[cp];
+        const F p_m = (F)pp[cm], p_0 = (F)pp[c], p_p = (F)pp[cp];
+        const F nxt = (F)b[(size_t)r * cols + c];
         // hornSchunck.cpp:27-28 (Sobel ksize 3) and :39; exact for 8-bit data
-        const float dx = (m_p - m_m) + 2.0f * (z_p - z_m) + (p_p - p_m);
-        const float dy = (p_m - m_m) + 2.0f * (p_0 - m_0) + (p_p - m_p);
-        const float dt = nxt - z_0;
+        const F dx = (m_p - m_m) + (F)2 * (z_p - z_m) + (p_p - p_m);
+        const F dy = (p_m - m_m) + (F)2 * (p_0 - m_0) + (p_p - m_p);
+        const F dt = nxt - z_0;
         const size_t o = blockIdx.z * plane + (size_t)r * cols + c;
-        gx[o] = dx;
-        gy[o] = dy;
-        gt[o] = dt;
+        gx[o] = (float)dx;
+        gy[o] = (float)dy;
+        gt[o] = (float)dt;
         // packed form is exact iff both frames are integers in [0, 255]
-        bad = !(z_0 == rintf(z_0) && nxt == rintf(nxt) && z_0 >= 0.f && z_0 <= 255.f &&
-                nxt >= 0.f && nxt <= 255.f);
+        bad = !(z_0 == rint(z_0) && nxt == rint(nxt) && z_0 >= (F)0 && z_0 <= (F)255 &&
+                nxt >= (F)0 && nxt <= (F)255);
         gpack[o] = pack_grad((int)dx, (int)dy, (int)dt);
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[blockIdx.z], 1u);
@@ -891,6 +894,10 @@ hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int ro
     if (dtype_in == 0)
         hipLaunchKernelGGL(hs_gradients_kernel<uint8_t>, grd, blk, 0, s,
                            (const uint8_t *)I0, (const uint8_t *)I1, rows, cols, gpack,
+                           gx, gy, gt, flags);
+    else if (dtype_in == 2)  // HSFLOW_F64 (CV_64FC1 frames)
+        hipLaunchKernelGGL(hs_gradients_kernel<double>, grd, blk, 0, s,
+                           (const double *)I0, (const double *)I1, rows, cols, gpack,
                            gx, gy, gt, flags);
     else if (dtype_in == 3)  // HSFLOW_F16 (config 5 inputs)
         hipLaunchKernelGGL(hs_gradients_kernel<_Float16>, grd, blk, 0, s,

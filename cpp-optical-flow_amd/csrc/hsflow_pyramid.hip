@@ -100,6 +100,10 @@ hipError_t launch_pyrdown(const void *src, int dtype, int rows, int cols, int ba
         hipLaunchKernelGGL(hs_pyrdown_kernel<float>, grd, blk, 0, s, (const float *)src,
                            rows, cols, dst, r2, c2, flags);
         break;
+    case 2:  // HSFLOW_F64
+        hipLaunchKernelGGL(hs_pyrdown_kernel<double>, grd, blk, 0, s, (const double *)src,
+                           rows, cols, dst, r2, c2, flags);
+        break;
     case 3:
         hipLaunchKernelGGL(hs_pyrdown_kernel<_Float16>, grd, blk, 0, s,
                            (const _Float16 *)src, rows, cols, dst, r2, c2, flags);

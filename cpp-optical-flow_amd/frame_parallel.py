@@ -131,8 +131,10 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
 
     The point-to-point calls are issued in the same order on both ends of
     every link (all scatter groups, then the gather groups in group order),
-    which is what keeps RCCL's in-order matching free of deadlock: a rank
-    posts its receives for every group before its first result send.
+    one batch per group on both ends, which is what keeps RCCL's in-order
+    matching free of deadlock: a rank posts its receives for every group
+    before its first result send.  (Verified with gloo, world 2 and 3; the
+    RCCL schedule runs first on the driver's multi-GPU node.)
     Returns rank 0's (u, v) list in stream order (None elsewhere, or when
     gather=False).  Bit-identical to run_stream: only the schedule changes."""
     mine = my_pairs(n_pairs, rank, world)
@@ -146,19 +148,22 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
         return out if gather else None
     groups = {r: chunk_split(my_pairs(n_pairs, r, world), chunks) for r in range(world)}
     n_groups = max(len(g) for g in groups.values())
-    # 1. scatter: every group of every rank posted up front, group-major
+    # 1. scatter: every group of every rank posted up front, group-major;
+    #    one batch per (group, destination), mirroring the receivers' one
+    #    batch per group, so RCCL's in-order matching pairs batches 1:1
     recv_groups: List[Tuple[torch.Tensor, torch.Tensor, list]] = []
     if rank == 0:
-        ops = []
+        scatter_reqs = []
         for c in range(n_groups):
             for dst in range(1, world):
                 if c >= len(groups[dst]):
                     continue
+                ops = []
                 for j in groups[dst][c]:
                     I0, I1 = stream[j]
                     ops.append(dist.P2POp(dist.isend, I0.to(device).contiguous(), dst))
                     ops.append(dist.P2POp(dist.isend, I1.to(device).contiguous(), dst))
-        scatter_reqs = dist.batch_isend_irecv(ops) if ops else []
+                scatter_reqs.extend(dist.batch_isend_irecv(ops))
     else:
         for grp in groups[rank]:
             a = torch.empty((len(grp),) + tuple(shape), dtype=dtype, device=device)

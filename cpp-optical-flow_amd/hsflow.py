@@ -294,9 +294,15 @@ def download_device(dst, src, stream=None):
         raise HsflowError(HSFLOW_ERR_ARG, "download sizes differ")
     if not (src.is_contiguous() and dst.is_contiguous()):
         raise HsflowError(HSFLOW_ERR_ARG, "download tensors must be contiguous")
-    _check(lib().hsflow_download_device(dst.data_ptr(), src.data_ptr(),
-                                        src.numel() * src.element_size(),
-                                        _stream_ptr(stream, src.device)))
+    # a pageable dst would silently serialise the 'overlapped' copy, and a
+    # CUDA dst would get a device-to-host copy kind on a device pointer
+    if not src.is_cuda or dst.is_cuda or not dst.is_pinned():
+        raise HsflowError(HSFLOW_ERR_ARG,
+                          "download_device: src must be a CUDA tensor, dst pinned host memory")
+    with _on(src.device):
+        _check(lib().hsflow_download_device(dst.data_ptr(), src.data_ptr(),
+                                            src.numel() * src.element_size(),
+                                            _stream_ptr(stream, src.device)))
 
 
 def flow_multi(devices, pairs, window: int, iters: int, alpha: float,
@@ -382,11 +388,19 @@ def compute(I0, I1, alpha: float, nIter: int, windowSize: int = 5, levels: int =
 # ------------------------------------------------------------ device (torch)
 def _stream_ptr(stream, device=None):
     """hipStream_t of `stream`, or of the current stream of `device` (the
-    tensors' device) when stream is None; the library runs each call on the
-    device its stream belongs to."""
+    tensors' device) when stream is None.  The library runs a call on the
+    device its stream belongs to; the null stream (torch's default stream is
+    0 on every device) means the CURRENT device, so every wrapper below makes
+    the tensors' device current around its library call (_on)."""
     if stream is None:
         return torch.cuda.current_stream(device).cuda_stream if torch is not None else None
     return getattr(stream, "cuda_stream", stream)
+
+
+def _on(device):
+    """Context that makes `device` current for one library call (a null
+    stream runs on the current device, include/hsflow.h)."""
+    return torch.cuda.device(device)
 
 
 def build_flags() -> int:
@@ -413,8 +427,10 @@ def _tensor_dtype(t) -> int:
         return F32
     if t.dtype == torch.float16:
         return F16
+    if t.dtype == torch.float64:
+        return F64
     raise HsflowError(HSFLOW_ERR_ARG,
-                      f"device input dtype {t.dtype} (want uint8/float16/float32)")
+                      f"device input dtype {t.dtype} (want uint8/float16/float32/float64)")
 
 
 def _check_dense(t, shape, name):
@@ -451,10 +467,11 @@ def flow_device(I0, I1, window: int, iters: int, alpha: float, u=None, v=None,
     _check_plane(v, (rows, cols), batch, "v")
     if workspace is None:
         workspace = alloc_workspace(rows, cols, batch, I0.device)
-    rc = lib().hsflow_flow_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0), rows,
-                                  cols, batch, int(window), int(iters), float(alpha),
-                                  u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
-                                  workspace.numel(), _stream_ptr(stream, I0.device))
+    with _on(I0.device):
+        rc = lib().hsflow_flow_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0), rows,
+                                      cols, batch, int(window), int(iters), float(alpha),
+                                      u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
+                                      workspace.numel(), _stream_ptr(stream, I0.device))
     _check(rc)
     return u, v
 
@@ -489,11 +506,12 @@ def flow_pyramid_device(I0, I1, levels: int, window: int, iters: int, alpha: flo
     if workspace is None:
         n = pyramid_workspace_bytes(rows, cols, batch, levels)
         workspace = torch.empty(n, dtype=torch.uint8, device=I0.device)
-    rc = lib().hsflow_flow_pyramid_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
-                                          rows, cols, batch, int(levels), int(window),
-                                          int(iters), float(alpha), u.data_ptr(),
-                                          v.data_ptr(), workspace.data_ptr(),
-                                          workspace.numel(), _stream_ptr(stream, I0.device))
+    with _on(I0.device):
+        rc = lib().hsflow_flow_pyramid_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
+                                              rows, cols, batch, int(levels), int(window),
+                                              int(iters), float(alpha), u.data_ptr(),
+                                              v.data_ptr(), workspace.data_ptr(),
+                                              workspace.numel(), _stream_ptr(stream, I0.device))
     _check(rc)
     return u, v
 
@@ -516,10 +534,11 @@ def pyramid_build_device(I0, I1, levels: int, workspace=None, stream=None):
     n = max(1, levels - 1)
     a0 = (_vp * n)(*[t.data_ptr() for t in P0]) if P0 else (_vp * 1)()
     a1 = (_vp * n)(*[t.data_ptr() for t in P1]) if P1 else (_vp * 1)()
-    _check(lib().hsflow_pyramid_build_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
-                                             rows, cols, batch, int(levels), a0, a1,
-                                             workspace.data_ptr(), workspace.numel(),
-                                             _stream_ptr(stream, I0.device)))
+    with _on(I0.device):
+        _check(lib().hsflow_pyramid_build_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
+                                                 rows, cols, batch, int(levels), a0, a1,
+                                                 workspace.data_ptr(), workspace.numel(),
+                                                 _stream_ptr(stream, I0.device)))
     return P0, P1
 
 
@@ -531,9 +550,10 @@ def upflow_device(uc, vc, u, v, stream=None):
     for t, name, shape in ((uc, "uc", (rc, cc)), (vc, "vc", (rc, cc)), (u, "u", (rows, cols)),
                            (v, "v", (rows, cols))):
         _check_plane(t, shape, 1, name)
-    _check(lib().hsflow_upflow_device(uc.data_ptr(), vc.data_ptr(), rc, cc, u.data_ptr(),
-                                      v.data_ptr(), rows, cols, 1,
-                                      _stream_ptr(stream, u.device)))
+    with _on(u.device):
+        _check(lib().hsflow_upflow_device(uc.data_ptr(), vc.data_ptr(), rc, cc, u.data_ptr(),
+                                          v.data_ptr(), rows, cols, 1,
+                                          _stream_ptr(stream, u.device)))
 
 
 def gradients_device(I0, I1, workspace, gx=None, gy=None, gt=None, stream=None):
@@ -542,10 +562,11 @@ def gradients_device(I0, I1, workspace, gx=None, gy=None, gt=None, stream=None):
     _check_dense(I0, (rows, cols), "I0")
     _check_dense(I1, (rows, cols), "I1")
     ptr = (lambda t: t.data_ptr() if t is not None else None)
-    rc = lib().hsflow_gradients_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
-                                       rows, cols, batch, ptr(gx), ptr(gy), ptr(gt),
-                                       workspace.data_ptr(), workspace.numel(),
-                                       _stream_ptr(stream, I0.device))
+    with _on(I0.device):
+        rc = lib().hsflow_gradients_device(I0.data_ptr(), I1.data_ptr(), _tensor_dtype(I0),
+                                           rows, cols, batch, ptr(gx), ptr(gy), ptr(gt),
+                                           workspace.data_ptr(), workspace.numel(),
+                                           _stream_ptr(stream, I0.device))
     _check(rc)
 
 
@@ -553,10 +574,11 @@ def jacobi_device(rows, cols, batch, window, iters, alpha, u, v, workspace,
                   warm_start=False, stream=None):
     _check_plane(u, (rows, cols), batch, "u")
     _check_plane(v, (rows, cols), batch, "v")
-    rc = lib().hsflow_jacobi_device(int(rows), int(cols), int(batch), int(window),
-                                    int(iters), float(alpha), int(bool(warm_start)),
-                                    u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
-                                    workspace.numel(), _stream_ptr(stream, u.device))
+    with _on(u.device):
+        rc = lib().hsflow_jacobi_device(int(rows), int(cols), int(batch), int(window),
+                                        int(iters), float(alpha), int(bool(warm_start)),
+                                        u.data_ptr(), v.data_ptr(), workspace.data_ptr(),
+                                        workspace.numel(), _stream_ptr(stream, u.device))
     _check(rc)
 
 
@@ -619,8 +641,9 @@ def bgr_to_gray_device(bgr, gray=None, stream=None):
             gray.numel() < batch * rows * cols or gray.device != bgr.device:
         raise HsflowError(HSFLOW_ERR_ARG, "gray: need a contiguous uint8 CUDA tensor of "
                           f"{batch} x {rows} x {cols} on {bgr.device}")
-    _check(lib().hsflow_bgr_to_gray_device(bgr.data_ptr(), rows, cols, batch,
-                                           gray.data_ptr(), _stream_ptr(stream, bgr.device)))
+    with _on(bgr.device):
+        _check(lib().hsflow_bgr_to_gray_device(bgr.data_ptr(), rows, cols, batch,
+                                               gray.data_ptr(), _stream_ptr(stream, bgr.device)))
     return gray
 
 

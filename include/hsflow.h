@@ -86,7 +86,9 @@ void *hsflow_stream(hsflow_ctx *ctx);
  * type dtype_in, row steps in BYTES, one per frame (cv::Mat::step of
  * imagePrev and imageNext; non-continuous ROIs ok, the two may differ).
  * u/v: rows x cols of dtype_out (HSFLOW_F64 = what the reference returns,
- * CV_64FC1, or HSFLOW_F32), row step out_step bytes. */
+ * CV_64FC1, or HSFLOW_F32), row step out_step bytes.  Frames are uploaded as
+ * they are; CV_64FC1 frames get their Sobel sums in float64 on the device
+ * (hornSchunck.cpp:23-28), each gradient rounded to f32 once. */
 int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
                 int rows, int cols, size_t in_step0, size_t in_step1, int window,
                 int iters, double alpha, void *u, void *v, int dtype_out,
@@ -100,7 +102,9 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
  * solved on devices[j % n_devices], each listed device by its own host
  * thread, context and stream, exactly as hsflow_flow (same bits).  A device
  * may be listed twice (two streams on one GPU).  Blocking; returns the
- * first error, its message in hsflow_last_error(NULL). */
+ * first error, its message in hsflow_last_error(NULL).  The per-device
+ * contexts are kept by the library across calls (no allocation or device
+ * synchronisation per call once warm); concurrent calls are serialised. */
 int hsflow_flow_multi(const int *devices, int n_devices, int batch,
                       const void *const *I0, const void *const *I1, int dtype_in, int rows,
                       int cols, size_t in_step0, size_t in_step1, int window, int iters,
@@ -115,9 +119,10 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
 /* ---- device pointers, stream-ordered ------------------------------------
  * A batch is `batch` (1..65535) independent frame pairs stored back to back:
  * I0[b][rows][cols], dense (pitch = cols elements), likewise u, v.
- * Inputs are U8, F16 or F32.  Outputs are f32.  `stream` is a hipStream_t (NULL =
- * default stream of the current device); the call runs on the device the
- * stream belongs to, whatever device is current.  `workspace` is device memory of at least
+ * Inputs are U8, F16, F32 or F64.  Outputs are f32.  `stream` is a hipStream_t
+ * (NULL = the default stream of the CURRENT device: then the caller must
+ * make the buffers' device current); a non-null stream's own device runs the
+ * call, whatever device is current.  `workspace` is device memory of at least
  * hsflow_workspace_bytes(rows, cols, batch) bytes, 256-byte aligned. */
 size_t hsflow_workspace_bytes(int rows, int cols, int batch);
 

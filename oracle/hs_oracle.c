@@ -243,7 +243,7 @@ void hso_flow_pyramid(const double *I0, const double *I1, int rows, int cols,
 
 static int sgn(int x) { return x < 0 ? -1 : (x > 0 ? 1 : 0); } /* :24-28 */
 
-/* :30-37  note: writes [0]=r,[1]=g,[2]=b into BGR memory, and only when
+/* plotFlow.cpp:24-32  note: writes [0]=r,[1]=g,[2]=b into BGR memory, and only when
  * 0 <= x < rows-1 and 0 <= y < cols-1 (the reference's off-by-one kept). */
 static void set_pixel(uint8_t *img, int rows, int cols, int x, int y, int r, int g,
                       int b) {
@@ -257,7 +257,7 @@ static void set_pixel(uint8_t *img, int rows, int cols, int x, int y, int r, int
     }
 }
 
-/* :40-47 */
+/* plotFlow.cpp:34-41 */
 static void move_lateral(int *x, int *y, double *R, int sx, int sy, int dx, int dy) {
     *x += sx;
     *R += dy;
@@ -267,7 +267,7 @@ static void move_lateral(int *x, int *y, double *R, int sx, int sy, int dx, int 
     }
 }
 
-/* :49-72 */
+/* plotFlow.cpp:43-66 */
 static void bresenham(uint8_t *img, int rows, int cols, int x0, int y0, int x1,
                       int y1, int r, int g, int b) {
     int dX = x1 - x0, dY = y1 - y0;
@@ -290,7 +290,7 @@ static void bresenham(uint8_t *img, int rows, int cols, int x0, int y0, int x1,
     }
 }
 
-/* :74-94 (namedWindow/imshow/imwrite left to the caller). */
+/* plotFlow.cpp:68-88 (namedWindow/imshow/imwrite left to the caller). */
 void hso_plot_bresenham(uint8_t *bgr, int rows, int cols, const double *u,
                         const double *v, int delta, float scale, int outlier) {
     for (int x1 = 0; x1 < rows; x1 += delta) {

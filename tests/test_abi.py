@@ -4,6 +4,7 @@ No GPU compute here."""
 import ctypes
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -97,7 +98,7 @@ def test_jacobi_kernel_selector():
     with pytest.raises(hsflow.HsflowError):
         hsflow.set_strip_options(-1)
     with pytest.raises(hsflow.HsflowError):
-        hsflow.lib().hsflow_set_strip_options(0, 2) and hsflow._check(-1)
+        hsflow._check(hsflow.lib().hsflow_set_strip_options(0, 2))
     hsflow.set_strip_options(48, False)
     hsflow.set_strip_options(0, True)
 
@@ -111,8 +112,8 @@ def test_device_entry_points_validate_before_touching_the_gpu():
                                   None) == hsflow.HSFLOW_ERR_ARG
     assert L.hsflow_jacobi_device(10, 10, 1, 5, 1, 1.0, 0, 1, 1, 1, 16,
                                   None) == hsflow.HSFLOW_ERR_ARG  # workspace too small
-    assert L.hsflow_gradients_device(1, 1, 2, 10, 10, 1, None, None, None, 1, 10 ** 6,
-                                     None) == hsflow.HSFLOW_ERR_ARG  # F64 on device
+    assert L.hsflow_gradients_device(1, 1, 7, 10, 10, 1, None, None, None, 1, 10 ** 6,
+                                     None) == hsflow.HSFLOW_ERR_ARG  # unknown dtype
 
 
 def test_flow_multi_validates_before_touching_the_gpu():
@@ -212,3 +213,36 @@ def test_batch_and_plane_limits_are_rejected_on_the_host():
     assert hsflow.workspace_bytes(1 << 14, 1 << 15, 1) == 0        # 2^29 px: offsets overflow
     assert hsflow.workspace_bytes(4 * 65535, 8, 1) > 0             # tallest plane
     assert hsflow.workspace_bytes(4 * 65535 + 1, 8, 1) == 0        # gridDim.y of K1
+
+
+def test_integration_c_snippets_compile(tmp_path):
+    """Every ```c block of INTEGRATION.md compiles against include/hsflow.h
+    (gcc, C99, warnings as errors): a snippet with a stale argument list --
+    e.g. one row step where the v2.0 ABI takes two -- fails here."""
+    import re
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```c\n(.*?)```", text, re.S)
+    assert blocks, "no C snippets found"
+    # the names the snippets use, declared as a caller would have them
+    pre = """#include <stddef.h>
+#include <stdint.h>
+#include "hsflow.h"
+void snippet(void);
+void snippet(void) {
+    int rows = 375, cols = 1242, batch = 1;
+    size_t prev_step = 1242, next_step = 1242, bgr_prev_step = 3726, bgr_next_step = 3726;
+    const uint8_t *prev = 0, *next = 0, *bgr_prev = 0, *bgr_next = 0;
+    double *u = 0, *v = 0;
+    void *stream = 0, *workspace = 0;
+    hsflow_ctx *ctx = 0;
+    (void)ctx; (void)rows; (void)cols; (void)batch; (void)prev_step; (void)next_step;
+    (void)bgr_prev_step; (void)bgr_next_step; (void)prev; (void)next; (void)bgr_prev;
+    (void)bgr_next; (void)u; (void)v; (void)stream; (void)workspace;
+"""
+    for k, b in enumerate(blocks):
+        src = tmp_path / f"snippet{k}.c"
+        src.write_text(pre + "{\n" + b + "\n}\n}\n")
+        out = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-Wno-unused-variable",
+                              "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
+                             capture_output=True, text=True)
+        assert out.returncode == 0, f"INTEGRATION.md C snippet {k}:\n{b}\n{out.stderr}"
