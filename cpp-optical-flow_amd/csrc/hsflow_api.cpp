@@ -50,8 +50,6 @@ int g_kb_override = 0;
 int g_kernel_override = 0;
 // K4 rows per segment (hsflow_set_strip_rows): 0 = automatic
 int g_strip_rows = 0;
-// K4 passes alternate their streaming direction (hsflow_set_strip_options)
-int g_strip_dir_alt = 1;
 
 // Kernel and blocking depth of a launch's passes.  K4 (streaming strips)
 // runs the full-depth passes when it is built for the window's default
@@ -338,7 +336,6 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         a.v_in = src_v;
         a.u_out = dst_is_user(pass) ? u : w.u2;
         a.v_out = dst_is_user(pass) ? v : w.v2;
-        a.strip_up = g_strip_dir_alt ? (pass & 1) : 0;
         hipError_t e = (strip && a.iters == kb)
                            ? hsflow::launch_jacobi_strip(a, window, kb, strip_rows, s)
                            : hsflow::launch_jacobi(a, window, kb, s);
@@ -707,11 +704,9 @@ int hsflow_set_jacobi_kernel(int k) {
     return HSFLOW_OK;
 }
 
-int hsflow_set_strip_options(int seg_rows, int alternate) {
-    if (seg_rows < 0 || seg_rows > kMaxRows || alternate < 0 || alternate > 1)
-        return HSFLOW_ERR_ARG;
+int hsflow_set_strip_rows(int seg_rows) {
+    if (seg_rows < 0 || seg_rows > kMaxRows) return HSFLOW_ERR_ARG;
     g_strip_rows = seg_rows;
-    g_strip_dir_alt = alternate;
     return HSFLOW_OK;
 }
 

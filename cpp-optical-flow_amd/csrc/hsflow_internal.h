@@ -19,7 +19,6 @@ struct JacobiArgs {
     const float *gx, *gy, *gt; // f32 gradients (non-integral inputs)
     const uint32_t *flags;     // per pair: 0 -> gpack valid, else f32 planes
     int seg_rows;              // K4 strip kernel: output rows per segment
-    int strip_up;              // K4: stream this pass upwards (odd passes)
 };
 
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,

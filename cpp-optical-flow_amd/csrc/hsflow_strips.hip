@@ -52,21 +52,20 @@ constexpr int kOOB = 0x7FFFFFF0;
 // K2's association (by image-row parity), w = 5: Q(t) = h(t) + h(t+1) at
 // odd t; M(y) = Q(y-1) + Q(y+1) at even y; S(y) = h(y-2) + M(y) for even y,
 // M(y-1) + h(y+2) for odd y.  w = 3: Q(t) = h(t) + h(t+1) at even t;
-// S(y) = h(y-1) + Q(y) for even y, Q(y-1) + h(y+1) for odd y.
-// A pass streams its rows downwards (the arrival of h(t) completes the
-// window of y = t - AR) or upwards (completes y = t + A); the same sums
-// come out in either order, so both give K2's bits.
+// S(y) = h(y-1) + Q(y) for even y, Q(y-1) + h(y+1) for odd y.  Rows stream
+// downwards: the arrival of h(t) completes the window of y = t - AR.
+// (An upward stream -- the same sums in the mirrored order, same bits --
+// was built and measured 4 % slower on its own and when passes alternated
+// direction)
 //
-// w = 5, downwards.  State before an even arrival t: e0 = h(t-4),
-// e1 = h(t-2), q = Q(t-3), x = h(t-1); before an odd arrival: x = M(t-3).
-// w = 5, upwards.  State before an odd arrival t: e0 = h(t+4),
-// e1 = h(t+2), q = Q(t+2), x = h(t+1); before an even arrival: x = M(t+2).
+// w = 5.  State before an even arrival t: e0 = h(t-4), e1 = h(t-2),
+// q = Q(t-3), x = h(t-1); before an odd arrival: x = M(t-3).
 struct VS5 {
     f2v e0, e1, q, x;
 };
-template <bool UP, int PT>  // PT: parity of the arriving image row t
+template <int PT>  // PT: parity of the arriving image row t
 __device__ __forceinline__ f2v vs_arrive(VS5 &s, f2v h) {
-    if constexpr (!UP && PT == 0) {
+    if constexpr (PT == 0) {
         const f2v qn = s.x + h;  // Q(t-1) = h(t-1) + h(t)
         const f2v m = s.q + qn;  // M(t-2) = Q(t-3) + Q(t-1)
         const f2v S = s.e0 + m;  // S(t-2) = h(t-4) + M(t-2)
@@ -75,52 +74,27 @@ __device__ __forceinline__ f2v vs_arrive(VS5 &s, f2v h) {
         s.q = qn;
         s.x = m;
         return S;
-    } else if constexpr (!UP) {
-        const f2v S = s.x + h;  // S(t-2) = M(t-3) + h(t)
-        s.x = h;
-        return S;
-    } else if constexpr (PT == 1) {
-        const f2v qn = h + s.x;  // Q(t) = h(t) + h(t+1)
-        const f2v m = qn + s.q;  // M(t+1) = Q(t) + Q(t+2)
-        const f2v S = m + s.e0;  // S(t+2) = M(t+1) + h(t+4)
-        s.e0 = s.e1;
-        s.e1 = h;
-        s.q = qn;
-        s.x = m;
-        return S;
     } else {
-        const f2v S = h + s.x;  // S(t+2) = h(t) + M(t+2)
+        const f2v S = s.x + h;  // S(t-2) = M(t-3) + h(t)
         s.x = h;
         return S;
     }
 }
-// w = 3, downwards.  State before an odd arrival t: h1 = h(t-1),
-// h2 = h(t-2); before an even arrival: q = Q(t-2).
-// w = 3, upwards.  State before an even arrival t: h1 = h(t+1),
-// h2 = h(t+2); before an odd arrival: q = Q(t+1).
+// w = 3.  State before an odd arrival t: h1 = h(t-1), h2 = h(t-2); before
+// an even arrival: q = Q(t-2).
 struct VS3 {
     f2v h1, h2, q;
 };
-template <bool UP, int PT>
+template <int PT>
 __device__ __forceinline__ f2v vs_arrive(VS3 &s, f2v h) {
-    if constexpr (!UP && PT == 1) {
+    if constexpr (PT == 1) {
         const f2v qn = s.h1 + h;  // Q(t-1) = h(t-1) + h(t)
         const f2v S = s.h2 + qn;  // S(t-1) = h(t-2) + Q(t-1)
         s.q = qn;
         s.h2 = h;
         return S;
-    } else if constexpr (!UP) {
-        const f2v S = s.q + h;  // S(t-1) = Q(t-2) + h(t)
-        s.h1 = h;
-        return S;
-    } else if constexpr (PT == 0) {
-        const f2v qn = h + s.h1;  // Q(t) = h(t) + h(t+1)
-        const f2v S = qn + s.h2;  // S(t+1) = Q(t) + h(t+2)
-        s.q = qn;
-        s.h2 = h;
-        return S;
     } else {
-        const f2v S = h + s.q;  // S(t+1) = h(t) + Q(t+1)
+        const f2v S = s.q + h;  // S(t-1) = Q(t-2) + h(t)
         s.h1 = h;
         return S;
     }
@@ -197,14 +171,14 @@ __device__ __forceinline__ void hrow(f2v u, f2v v, f2v &hu, f2v &hv) {
 }  // namespace
 
 // Segment body: rows [a, b) of strip columns [c0, c0 + 128) of one pair,
-// streamed downwards or (UP) upwards.  U = unroll period (multiple of the
-// operator ring KB*AR, of 2 and of D).
-template <int W, int KB, int D, int U, bool X2, bool G32, bool UP>
+// streamed downwards.  U = unroll period (multiple of the operator ring
+// KB*AR, of 2 and of D).
+template <int W, int KB, int D, int U, bool X2, bool G32>
 __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, int plane_bytes,
                                            int c0, int a, int b) {
     constexpr int A = W - W / 2 - 1, AR = W / 2;
     static_assert(A == AR, "K4 is built for odd windows");
-    constexpr int L = KB * AR;  // operator ring: the rows t -+ AR .. t -+ KB AR
+    constexpr int L = KB * AR;  // operator ring: the rows t - AR .. t - KB AR
     static_assert(U % L == 0 && U % 2 == 0 && U % D == 0, "unroll period");
     using VS = typename VSOf<W>::type;
     constexpr int HLc = KB * A + ((KB * A) & 1), HRc = KB * AR + ((KB * AR) & 1);
@@ -244,13 +218,10 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                                               0x00020000);
 
     const float alpha2 = p.alpha2;
-    // first and last input row of the stream; the first is even (segment
-    // starts are even, and so is KB A; an upward stream starts one row
-    // lower when needed: a real row below only widens the complete part of
-    // its windows)
-    const int t_first = UP ? ((b - 1 + KB * AR) + 1) & ~1 : a - KB * A;
-    const int t_last = UP ? a - KB * A : b - 1 + KB * AR;
-    constexpr int dir = UP ? -1 : 1;
+    // first and last input row of the stream (the first is even: segment
+    // starts are even, and so is KB A)
+    const int t_first = a - KB * A;
+    const int t_last = b - 1 + KB * AR;
     auto issue = [&](RowIn<G32> &d, int r) {
         const bool rin = (unsigned)r < (unsigned)rows;
         const int so = rin ? r * cols * 4 : 0;
@@ -259,7 +230,7 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
 
     RowIn<G32> buf[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) issue(buf[k], t_first + dir * k);
+    for (int k = 0; k < D; ++k) issue(buf[k], t_first + k);
 
     const f2v z = {0.f, 0.f};
     f2v OX[L], OY[L], OT[L];
@@ -284,28 +255,28 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
         constexpr bool ROWE = decltype(rowe_c)::value;
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            const int t = tb + dir * k;
+            const int t = tb + k;
             // 1. this row's input (loaded D steps ago), then the load of
-            //    row t + D (t - D upwards) into the freed slot
+            //    row t + D into the freed slot
             const RowIn<G32> cur = buf[k % D];
-            issue(buf[k % D], t + dir * D);
+            issue(buf[k % D], t + D);
             // 2. level-0 horizontal sums of row t
             f2v hu, hv;
             hrow<W>(cur.u, cur.v, hu, hv);
-            // 3. the stages: stage j (1-based) receives row t -+ (j-1) AR of
-            //    iteration j-1 and updates row t -+ j AR to iteration j
+            // 3. the stages: stage j (1-based) receives row t - (j-1) AR of
+            //    iteration j-1 and updates row t - j AR to iteration j
 #pragma unroll
             for (int j = 0; j < KB; ++j) {
-                const int y = t - dir * (j + 1) * AR;
-                // image-row parity of the arriving row t -+ j AR (tb even)
+                const int y = t - (j + 1) * AR;
+                // image-row parity of the arriving row t - j AR (tb even)
                 const int pt = (k + j * AR) & 1;
                 f2v Su, Sv;
                 if (pt == 0) {
-                    Su = vs_arrive<UP, 0>(su[j], hu);
-                    Sv = vs_arrive<UP, 0>(sv[j], hv);
+                    Su = vs_arrive<0>(su[j], hu);
+                    Sv = vs_arrive<0>(sv[j], hv);
                 } else {
-                    Su = vs_arrive<UP, 1>(su[j], hu);
-                    Sv = vs_arrive<UP, 1>(sv[j], hv);
+                    Su = vs_arrive<1>(su[j], hu);
+                    Sv = vs_arrive<1>(sv[j], hv);
                 }
                 const int sl = ((k - (j + 1) * AR) % L + L) % L;  // operator slot of row y
                 f2v nu, nv;
@@ -347,35 +318,13 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // three loops, so the blocks whose stage rows all lie inside the image
     // run a body without row zeroing (one body per loop: a two-body loop
     // makes the allocator spill); the rarely used variants take one loop
-    auto more = [&](int tb) { return UP ? tb >= t_last : tb <= t_last; };
-    // the block's stage rows: downwards [tb - KB AR, tb + U - 1 - AR],
-    // upwards [tb - (U - 1) + A, tb + KB A]
-    auto edge_first = [&](int tb) { return UP ? tb + KB * A >= rows : tb - KB * AR < 0; };
-    auto inside_end = [&](int tb) {
-        return UP ? tb - (U - 1) + A >= 0 : tb + U - 1 - AR < rows;
-    };
+    // (the block's stage rows are [tb - KB AR, tb + U - 1 - AR])
     int tb = t_first;
     if constexpr (X2 && !G32) {
-        for (; more(tb) && edge_first(tb); tb += dir * U) block(tb, std::true_type{});
-        for (; more(tb) && inside_end(tb); tb += dir * U) block(tb, std::false_type{});
+        for (; tb <= t_last && tb - KB * AR < 0; tb += U) block(tb, std::true_type{});
+        for (; tb <= t_last && tb + U - 1 - AR < rows; tb += U) block(tb, std::false_type{});
     }
-    for (; more(tb); tb += dir * U) block(tb, std::true_type{});
-}
-
-template <int W, int KB, int D, int U, bool UP>
-__device__ __forceinline__ void strip_variant(const JacobiArgs &p, size_t pbase,
-                                              int plane_bytes, int c0, int a, int b, bool g32) {
-    if (g32) {
-        if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, true, UP>(p, pbase, plane_bytes, c0, a, b);
-        else
-            strip_body<W, KB, D, U, false, true, UP>(p, pbase, plane_bytes, c0, a, b);
-    } else {
-        if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, false, UP>(p, pbase, plane_bytes, c0, a, b);
-        else
-            strip_body<W, KB, D, U, false, false, UP>(p, pbase, plane_bytes, c0, a, b);
-    }
+    for (; tb <= t_last; tb += U) block(tb, std::true_type{});
 }
 
 // ---------------------------------------------------------------- kernel
@@ -405,13 +354,17 @@ __global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs
     const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)p.cols;
     const int plane_bytes = p.rows * p.cols * 4;
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
-    // successive passes stream in opposite directions: the rows a pass
-    // wrote last are the first the next one reads, while they may still be
-    // in the Infinity Cache
-    if (p.strip_up)
-        strip_variant<W, KB, D, U, true>(p, pbase, plane_bytes, c0, a, b, g32);
-    else
-        strip_variant<W, KB, D, U, false>(p, pbase, plane_bytes, c0, a, b, g32);
+    if (g32) {
+        if ((p.cols & 1) == 0)
+            strip_body<W, KB, D, U, true, true>(p, pbase, plane_bytes, c0, a, b);
+        else
+            strip_body<W, KB, D, U, false, true>(p, pbase, plane_bytes, c0, a, b);
+    } else {
+        if ((p.cols & 1) == 0)
+            strip_body<W, KB, D, U, true, false>(p, pbase, plane_bytes, c0, a, b);
+        else
+            strip_body<W, KB, D, U, false, false>(p, pbase, plane_bytes, c0, a, b);
+    }
 }
 
 // ------------------------------------------------------------- launcher
@@ -424,13 +377,15 @@ template <> struct StripCfg<3, 8> { static constexpr int D = 2, U = 8; };
 bool strip_supported(int W, int KB) { return (W == 5 && KB == 6) || (W == 3 && KB == 8); }
 
 // Segment rows for a launch.  Each wave streams N rows plus the KB (W - 1)
-// halo rows its stages need, so tall segments waste little work and few
-// re-read rows, while short ones give more waves.  Policy (measured, DESIGN.md
-// §4 K4): the shortest segment of at least 72 rows -- with N + KB (W - 1)
-// a multiple of the unroll period -- whose waves fit one round of the
-// chip's slots (two waves per SIMD); if even the tallest sensible one (240
-// rows) needs several rounds, the height with the fewest rounds x steps.
-// `override_rows` > 0 forces N (rounded up to the period).
+// halo rows its stages need: tall segments waste little work and re-read
+// few rows, short ones give more waves.  Cost model (fitted to same-box
+// sweeps): a wave alone on its SIMD takes ~0.45 us per
+// streamed row, two waves sharing a SIMD ~0.75 us each; a launch's waves
+// come in rounds of 2 per SIMD (the last round at 1 per SIMD if it has at
+// most one wave per SIMD); the pass cannot beat its row loads (1.5 KB per
+// wave-row) at ~5 TB/s.  Candidates: N >= 48 with N + KB (W - 1) a
+// multiple of the unroll period, up to 240 rows.  `override_rows` > 0
+// forces N (rounded up to the period).
 int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int *nseg_out,
                    int *nstrips_out, int override_rows) {
     const int A = W - W / 2 - 1, AR = W / 2;
@@ -444,21 +399,24 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
         while ((n + halo) % U != 0 || (n & 1)) ++n;
         return n;
     };
-    auto waves = [&](int n) { return strips * ((rows + n - 1) / n); };
-    int best_n = aligned(override_rows > 0 ? override_rows : 72);
-    if (override_rows <= 0 && waves(best_n) > slots) {
-        long best = -1;
-        for (int n = best_n; n <= 240; n = aligned(n + 1)) {
-            const long w = waves(n);
-            if (w <= slots) {
-                best_n = n;
-                break;
-            }
-            const long t = (w + slots - 1) / slots * (n + halo);
-            if (best < 0 || t < best) {
+    int best_n = aligned(override_rows > 0 ? override_rows : 84);
+    if (override_rows <= 0) {
+        const long simds = slots / 2 > 0 ? slots / 2 : 1;
+        double best = -1.0;
+        for (int n = aligned(48); n <= 240; n = aligned(n + 1)) {
+            const long w = strips * ((rows + n - 1) / n);
+            const long rounds = (w + slots - 1) / slots;
+            const long last = w - (rounds - 1) * slots;
+            const int steps = n + halo;
+            const double compute = (double)(rounds - 1) * steps * 0.75 +
+                                   (double)steps * (last <= simds ? 0.45 : 0.75);
+            const double mem = (double)w * steps * 1536.0 / 5e12 * 1e6;
+            const double t = compute > mem ? compute : mem;
+            if (best < 0 || t < best - 1e-9) {
                 best = t;
                 best_n = n;
             }
+            if (n >= rows) break;  // taller segments only repeat this one
         }
     }
     *nseg_out = (rows + best_n - 1) / best_n;
@@ -467,8 +425,9 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
 }
 
 // K4 pays when its waves, at the policy's segment height, fill a good part
-// of the chip (a single 1080p pair has 19 strips: ~285 waves for 2048
-// slots, and K2's tiles run it faster; a 4K pair's 37 strips fill 0.54).
+// of the chip (a single 1080p pair has 19 strips: ~250 waves for 2048
+// slots, and K2's tiles run it faster; a 4K pair's 37 strips, 962 waves of
+// 84 rows, run faster on K4).
 bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
     int nseg = 0, nstrips = 0;
     strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 0);

@@ -51,7 +51,7 @@ EXPORTS = (
     "hsflow_flow_pyramid_device", "hsflow_flow_pyramid", "hsflow_bgr_to_gray_device",
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
     "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
-    "hsflow_download_device", "hsflow_jacobi_kernel_name", "hsflow_set_strip_options",
+    "hsflow_download_device", "hsflow_jacobi_kernel_name", "hsflow_set_strip_rows",
 )
 BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
 
@@ -112,7 +112,7 @@ def lib():
     L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
     L.hsflow_set_max_streams.argtypes = [i]
     L.hsflow_set_jacobi_kernel.argtypes = [i]
-    L.hsflow_set_strip_options.argtypes = [i, i]
+    L.hsflow_set_strip_rows.argtypes = [i]
     L.hsflow_jacobi_kernel_name.argtypes = [i, i, i, i]
     L.hsflow_jacobi_kernel_name.restype = ctypes.c_char_p
     L.hsflow_pyramid_level_size.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
@@ -598,10 +598,9 @@ def set_jacobi_kernel(k: int):
     _check(lib().hsflow_set_jacobi_kernel(int(k)))
 
 
-def set_strip_options(seg_rows: int = 0, alternate: bool = True):
-    """K4 rows per segment (0 = automatic) and whether successive passes
-    alternate their streaming direction; identical bits for any choice."""
-    _check(lib().hsflow_set_strip_options(int(seg_rows), int(bool(alternate))))
+def set_strip_rows(seg_rows: int = 0):
+    """K4 rows per segment (0 = automatic); identical bits for any choice."""
+    _check(lib().hsflow_set_strip_rows(int(seg_rows)))
 
 
 def jacobi_kernel_name(rows, cols, batch, window) -> str:

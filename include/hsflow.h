@@ -156,12 +156,11 @@ int hsflow_iters_per_launch(int rows, int cols, int batch, int window);
  * identical bits.  Process-wide; not thread-safe against running solves. */
 int hsflow_set_jacobi_kernel(int k);
 
-/* K4 streaming passes: `seg_rows` = rows per segment (each wave streams
- * one segment of one 128-column strip), 0 = automatic (default);
- * `alternate` = 1 (default): successive passes stream in opposite
- * directions, 0: every pass top to bottom.  Results are bit-identical for
- * every choice.  Process-wide; not thread-safe against running solves. */
-int hsflow_set_strip_options(int seg_rows, int alternate);
+/* Rows per segment of the K4 streaming passes (each wave streams one
+ * segment of one 128-column strip); 0 = automatic (default, a cost model of
+ * waves per SIMD and row loads).  Results are bit-identical for every
+ * choice.  Process-wide; not thread-safe against running solves. */
+int hsflow_set_strip_rows(int seg_rows);
 
 /* Name of the kernel that runs the full-depth Jacobi passes of a solve of
  * this shape under the current settings ("hs_jacobi_strip_kernel",

@@ -96,11 +96,9 @@ def test_jacobi_kernel_selector():
     assert hsflow.jacobi_kernel_name(2160, 3840, 2, 5) == "hs_jacobi_strip_kernel"
     assert hsflow.jacobi_kernel_name(0, 10, 1, 5) == ""
     with pytest.raises(hsflow.HsflowError):
-        hsflow.set_strip_options(-1)
-    with pytest.raises(hsflow.HsflowError):
-        hsflow._check(hsflow.lib().hsflow_set_strip_options(0, 2))
-    hsflow.set_strip_options(48, False)
-    hsflow.set_strip_options(0, True)
+        hsflow.set_strip_rows(-1)
+    hsflow.set_strip_rows(48)
+    hsflow.set_strip_rows(0)
 
 
 def test_device_entry_points_validate_before_touching_the_gpu():
