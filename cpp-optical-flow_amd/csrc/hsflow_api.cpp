@@ -61,10 +61,14 @@ struct PassPlan {
     bool strip;
 };
 
+// K4's depth: the caller's (hsflow_set_iters_per_launch) or the window's default
+int strip_kb(int window) {
+    return g_kb_override > 0 ? g_kb_override : hsflow::default_kb(window);
+}
+
 bool strip_use(int window, int rows, int cols, int batch) {
-    const int kb = hsflow::default_kb(window);
+    const int kb = strip_kb(window);
     if (g_kernel_override == 2 || window > 9 || !hsflow::strip_supported(window, kb)) return false;
-    if (g_kb_override > 0 && g_kb_override != kb) return false;
     if (g_kernel_override == 4) return true;
     return rows > 0 && cols > 0 && batch > 0 &&
            hsflow::strip_fills(window, kb, rows, cols, batch, 8 * hsflow::device_cus());
@@ -160,7 +164,7 @@ bool device_dtype_ok(int dtype) {
 // split over side streams); 0 = shape unknown (no fill adjustment)
 PassPlan plan_passes(int window, bool need_f32, int rows = 0, int cols = 0, int batch = 0) {
     if (window > 9) return {1, false};
-    if (strip_use(window, rows, cols, batch)) return {hsflow::default_kb(window), true};
+    if (strip_use(window, rows, cols, batch)) return {strip_kb(window), true};
     if (g_kb_override > 0 && hsflow::kb_supported(window, g_kb_override, need_f32))
         return {g_kb_override, false};
     int kb = hsflow::fill_kb(window, hsflow::default_kb(window), rows, cols, batch);
@@ -336,9 +340,12 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         a.v_in = src_v;
         a.u_out = dst_is_user(pass) ? u : w.u2;
         a.v_out = dst_is_user(pass) ? v : w.v2;
+        // a K2 pass (a shorter last pass of a K4 solve) takes a depth K2 is
+        // built for: any depth >= its iterations gives the same bits
+        const int kb2 = hsflow::kb_supported(window, kb, maybe_f32) ? kb : a.iters;
         hipError_t e = (strip && a.iters == kb)
                            ? hsflow::launch_jacobi_strip(a, window, kb, strip_rows, s)
-                           : hsflow::launch_jacobi(a, window, kb, s);
+                           : hsflow::launch_jacobi(a, window, kb2, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "jacobi launch");
         src_u = a.u_out;
         src_v = a.v_out;

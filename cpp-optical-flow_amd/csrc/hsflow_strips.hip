@@ -145,19 +145,31 @@ __device__ __forceinline__ void load_row(RowIn<G32> &d, const Rsrc &rs, int vo_e
     }
 }
 
+// op_setup (hsflow_device.h) for the column pair in packed FP32: the same
+// operations per column -- fma(Ix, Ix, alpha^2), fma(Iy, Iy, .), rsq, three
+// products -- so the same bits, in half the instructions
 template <bool G32>
 __device__ __forceinline__ void row_op(float alpha2, const RowIn<G32> &d, f2v &X, f2v &Y,
                                        f2v &T) {
-    float ixe, iye, ite, ixo, iyo, ito;
+    f2v ix, iy, it;
     if constexpr (G32) {
-        ixe = d.gx.x; ixo = d.gx.y;
-        iye = d.gy.x; iyo = d.gy.y;
-        ite = d.gt.x; ito = d.gt.y;
+        ix = d.gx;
+        iy = d.gy;
+        it = d.gt;
     } else {
+        float ixe, iye, ite, ixo, iyo, ito;
         unpack_grad(d.g.x, ixe, iye, ite);
         unpack_grad(d.g.y, ixo, iyo, ito);
+        ix = f2v{ixe, ixo};
+        iy = f2v{iye, iyo};
+        it = f2v{ite, ito};
     }
-    op_setup(alpha2, ixe, iye, ite, ixo, iyo, ito, X, Y, T);
+    const f2v a2 = {alpha2, alpha2};
+    const f2v den = a2 + ix * ix + iy * iy;
+    const f2v sc = {__builtin_amdgcn_rsqf(den.x), __builtin_amdgcn_rsqf(den.y)};
+    X = ix * sc;
+    Y = iy * sc;
+    T = it * sc;
 }
 
 template <int W>
@@ -289,24 +301,29 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                 }
                 if (j + 1 < KB) {
                     hrow<W>(nu, nv, hu, hv);
-                } else if (y >= a && y < b) {
-                    const int so = y * cols * 4;
+                } else {
+                    // every step issues its two stores (out-of-segment rows
+                    // at an out-of-range offset, dropped): the compiler then
+                    // counts them in its vmcnt waits, which keep the loads
+                    // of the D rows ahead in flight
+                    const bool sin = y >= a && y < b;
+                    const int so = sin ? y * cols * 4 : 0;
+                    const int oe = sin ? st_e : kOOB;
                     if constexpr (X2) {
                         __builtin_amdgcn_raw_buffer_store_b64(
-                            u2v{__float_as_uint(nu.x), __float_as_uint(nu.y)}, rs.uo, st_e, so,
-                            2);
+                            u2v{__float_as_uint(nu.x), __float_as_uint(nu.y)}, rs.uo, oe, so, 2);
                         __builtin_amdgcn_raw_buffer_store_b64(
-                            u2v{__float_as_uint(nv.x), __float_as_uint(nv.y)}, rs.vo, st_e, so,
-                            2);
+                            u2v{__float_as_uint(nv.x), __float_as_uint(nv.y)}, rs.vo, oe, so, 2);
                     } else {
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.x), rs.uo, st_e,
-                                                              so, 2);
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.y), rs.uo, st_o,
-                                                              so, 2);
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.x), rs.vo, st_e,
-                                                              so, 2);
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.y), rs.vo, st_o,
-                                                              so, 2);
+                        const int oo = sin ? st_o : kOOB;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.x), rs.uo, oe, so,
+                                                              2);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.y), rs.uo, oo, so,
+                                                              2);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.x), rs.vo, oe, so,
+                                                              2);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.y), rs.vo, oo, so,
+                                                              2);
                     }
                 }
             }
@@ -424,14 +441,15 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
     return best_n;
 }
 
-// K4 pays when its waves, at the policy's segment height, fill a good part
-// of the chip (a single 1080p pair has 19 strips: ~250 waves for 2048
-// slots, and K2's tiles run it faster; a 4K pair's 37 strips, 962 waves of
-// 84 rows, run faster on K4).
+// K4 pays when its waves fill a good part of the chip with tall segments:
+// at least 0.45 of the wave slots with 84-row segments (same-box sweeps: a
+// 4K pair, 37 strips x 26 segments = 962 waves, runs K4 5 % faster than
+// K2; two 1080p pairs, 38 x 13 = 494 waves, and a single one, 247, run K2's
+// tiles 30 % faster).
 bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
     int nseg = 0, nstrips = 0;
-    strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 0);
-    return (long)nseg * nstrips * batch * 20 >= (long)slots * 7;  // >= 0.35 of the slots
+    strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 84);
+    return (long)nseg * nstrips * batch * 20 >= (long)slots * 9;  // >= 0.45 of the slots
 }
 
 // One K4 pass of `a.batch` pairs in segments of `seg_rows` rows (the

@@ -6,7 +6,7 @@ import csv, glob, json, os, statistics, sys
 d = sys.argv[1]
 scale = 2.0
 res = {}
-for kdir in sorted(glob.glob(os.path.join(d, "k*"))):
+for kdir in sorted(glob.glob(os.path.join(d, "*"))):
     if not os.path.isdir(kdir):
         continue
     k = os.path.basename(kdir)
@@ -31,7 +31,7 @@ for kdir in sorted(glob.glob(os.path.join(d, "k*"))):
     if "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
         r["hbm_MB"] = (ctr["FETCH_SIZE"] * 1024 * scale + ctr["WRITE_SIZE"] * 1024) / 1e6
         if "median_us" in r:
-            r["hbm_TBps"] = r["hbm_MB"] / r["median_us"] / 1e6 * 1e6 / 1e6
+            r["hbm_TBps"] = r["hbm_MB"] / r["median_us"]
     if "GRBM_GUI_ACTIVE" in ctr and "median_us" in r:
         r["clock_GHz"] = ctr["GRBM_GUI_ACTIVE"] / 8 / (r["median_us"] * 1e3)
         if "SQ_INSTS_VALU" in ctr:
@@ -41,6 +41,10 @@ for kdir in sorted(glob.glob(os.path.join(d, "k*"))):
         r["wait_any"] = ctr.get("SQ_WAIT_ANY", 0) / w
         r["wait_inst_any"] = ctr.get("SQ_WAIT_INST_ANY", 0) / w
         r["active_inst_any"] = ctr.get("SQ_ACTIVE_INST_ANY", 0) / w
+    for nm in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC",
+               "SQ_INST_CYCLES_VMEM"):
+        if nm in ctr and "SQ_WAVE_CYCLES" in ctr:
+            r[nm.lower() + "_frac"] = ctr[nm] / ctr["SQ_WAVE_CYCLES"]
     if "TCC_HIT_sum" in ctr:
         r["l2_hit"] = ctr["TCC_HIT_sum"] / max(1, ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"])
     res[k] = r

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--windows", default="5,3")
     ap.add_argument("--streams", type=int, default=0)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--kb", type=int, default=0, help="iterations per pass (0 auto)")
     a = ap.parse_args()
     cases = {"1080p8": (8, 1080, 1920, 300), "4k2": (2, 2160, 3840, 500),
              "1080p1": (1, 1080, 1920, 300), "4k1": (1, 2160, 3840, 500),
@@ -51,6 +52,7 @@ def main():
              "1080p2": (2, 1080, 1920, 300), "8k1": (1, 4320, 7680, 60),
              "1080p32": (32, 1080, 1920, 60)}
     hsflow.set_max_streams(a.streams)
+    hsflow.set_iters_per_launch(a.kb)
     for name in a.cases.split(","):
         batch, rows, cols, iters = cases[name]
         ps = [hsflow.synth_pair(1000 + i, rows, cols) for i in range(batch)]
@@ -61,7 +63,7 @@ def main():
             hsflow.set_jacobi_kernel(2)
             t2, u2 = timed(I0, I1, w, iters)
             hsflow.set_jacobi_kernel(0)
-            rec = {"tag": a.tag, "streams": a.streams, "case": name, "w": w, "k2_ms": round(t2 * 1e3, 3), "k2": round(mp / t2)}
+            rec = {"tag": a.tag, "kb": a.kb, "streams": a.streams, "case": name, "w": w, "k2_ms": round(t2 * 1e3, 3), "k2": round(mp / t2)}
             for n in [int(x) for x in a.rows_list.split(",")]:
                 hsflow.set_strip_rows(n)
                 t4, u4 = timed(I0, I1, w, iters)
