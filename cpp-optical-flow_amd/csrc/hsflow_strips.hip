@@ -234,11 +234,14 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // starts are even, and so is KB A)
     const int t_first = a - KB * A;
     const int t_last = b - 1 + KB * AR;
-    auto issue = [&](RowIn<G32> &d, int r) {
-        const bool rin = (unsigned)r < (unsigned)rows;
-        const int so = rin ? r * cols * 4 : 0;
-        load_row<X2, G32>(d, rs, rin ? launder(ld_e) : kOOB, rin ? launder(ld_o) : kOOB, so);
-    };
+    // Rows outside the image read 0 through the buffer range check, which
+    // covers voffset + soffset (gfx950; scripts/ubench/soffset_range.hip):
+    // the row's byte offset goes in soffset, 2^31 for rows above the image
+    // (no VALU work and no branches per load; a per-lane offset stays
+    // constant).  Offsets stay below 2^32: voffset < 2^31, soffset <= 2^31.
+    const int row_bytes = cols * 4;
+    auto row_off = [&](int r) { return r >= 0 ? r * row_bytes : (int)0x80000000; };
+    auto issue = [&](RowIn<G32> &d, int r) { load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(r)); };
 
     RowIn<G32> buf[D];
 #pragma unroll
@@ -307,15 +310,15 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                     // counts them in its vmcnt waits, which keep the loads
                     // of the D rows ahead in flight
                     const bool sin = y >= a && y < b;
-                    const int so = sin ? y * cols * 4 : 0;
-                    const int oe = sin ? st_e : kOOB;
+                    const int so = sin ? y * row_bytes : (int)0x80000000;
+                    const int oe = st_e;
                     if constexpr (X2) {
                         __builtin_amdgcn_raw_buffer_store_b64(
                             u2v{__float_as_uint(nu.x), __float_as_uint(nu.y)}, rs.uo, oe, so, 2);
                         __builtin_amdgcn_raw_buffer_store_b64(
                             u2v{__float_as_uint(nv.x), __float_as_uint(nv.y)}, rs.vo, oe, so, 2);
                     } else {
-                        const int oo = sin ? st_o : kOOB;
+                        const int oo = st_o;
                         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.x), rs.uo, oe, so,
                                                               2);
                         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.y), rs.uo, oo, so,
