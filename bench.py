@@ -330,7 +330,7 @@ def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
             "naive_B_per_px_iter": NAIVE_BYTES_PER_PX_ITER,
             "hbm_frac": None, "valu_frac": None}
     pmc = pmc_for(wl_name, window, batch, kb, kernel)
-    if pmc is not None:
+    if pmc is not None and pmc.get("hbm_bytes_per_launch"):
         traffic = pmc["hbm_bytes_per_launch"]
         roof["traffic"] = traffic
         roof["traffic_over_algorithmic"] = round(traffic / pass_bytes, 3)
