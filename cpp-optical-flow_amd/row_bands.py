@@ -115,11 +115,20 @@ class DeviceOps:
         self._ws = None
 
     def levels(self, I0, I1, L: int):
-        P0, P1 = self.hs.pyramid_build_device(I0, I1, L, stream=self.stream)
+        with self._on():
+            P0, P1 = self.hs.pyramid_build_device(I0, I1, L, stream=self.stream)
         return [I0] + P0, [I1] + P1
 
+    def _on(self):
+        """torch's own operations (allocation, fills, copies) go on the
+        rank's stream when it has one, in order with the library calls"""
+        import contextlib
+        return (contextlib.nullcontext() if self.stream is None
+                else self.torch.cuda.stream(self.stream))
+
     def zeros(self, r: int, c: int):
-        return self.torch.zeros((r, c), dtype=self.torch.float32, device=self.device)
+        with self._on():
+            return self.torch.zeros((r, c), dtype=self.torch.float32, device=self.device)
 
     def workspace(self, r: int, c: int):
         need = self.hs.workspace_bytes(r, c, 1)
@@ -142,18 +151,31 @@ class DeviceOps:
         self.hs.upflow_device(uc, vc, u, v, stream=self.stream)
 
     def set_zero(self, x):
-        x.zero_()
+        with self._on():
+            x.zero_()
 
     # overlapped schedule (solve_overlapped): the interior runs on a side
-    # stream, the edge strips and the exchange on the caller's stream
-    def clone(self, x):
-        return x.clone()
+    # stream, the edge strips and the exchange on the rank's stream
+    def stack(self, planes):
+        with self._on():
+            return self.torch.stack(planes)
 
-    def cat_rows(self, a, b):
-        return self.torch.cat([a, b], 0)
+    def copy_many(self, dsts, srcs):
+        with self._on():
+            self.torch._foreach_copy_(dsts, srcs)
 
-    def copy_rows(self, dst, src):
-        dst.copy_(src)
+    def gradients_own(self, J0, J1):
+        n, r, c = J0.shape
+        with self._on():
+            ws = self.torch.empty(self.hs.workspace_bytes(r, c, n), dtype=self.torch.uint8,
+                                  device=self.device)
+        self.hs.gradients_device(J0, J1, ws, stream=self.stream)
+        return ws
+
+    def jacobi_stack(self, ws, U, V, n: int, side: bool = False):
+        b, r, c = U.shape
+        self.hs.jacobi_device(r, c, b, self.window, n, self.alpha, U, V, ws,
+                              warm_start=True, stream=self._side if side else self.stream)
 
     def _main(self):
         return self.torch.cuda.current_stream(self.device) if self.stream is None else self.stream
@@ -163,11 +185,6 @@ class DeviceOps:
             self._side = self.torch.cuda.Stream(device=self.device)
         self._side.wait_stream(self._main())
 
-    def jacobi_side(self, ws, u, v, n: int):
-        r, c = u.shape
-        self.hs.jacobi_device(r, c, 1, self.window, n, self.alpha, u, v, ws,
-                              warm_start=True, stream=self._side)
-
     def join(self):
         self._main().wait_stream(self._side)
 
@@ -175,7 +192,10 @@ class DeviceOps:
 # -------------------------------------------------------------------- comm
 class LocalComm:
     """N virtual ranks in one process (tests, one-GPU rehearsal): the halo
-    exchange is a copy between the ranks' planes."""
+    exchange is a copy between the ranks' planes.  Virtual ranks that run
+    on streams of their own (DeviceOps(stream=...)) meet at the exchange:
+    the copies run once every rank's stream has reached it, and every rank's
+    stream continues after them (the ordering a real exchange gives)."""
 
     def start(self, states: Sequence["RankState"], level: int):
         self.exchange(states, level)
@@ -185,6 +205,41 @@ class LocalComm:
         pass
 
     def exchange(self, states: Sequence["RankState"], level: int):
+        self._met(states, lambda: self._copy_halos(states, level))
+
+    def start_strips(self, states: Sequence["RankState"]):
+        """The overlapped schedule's exchange: each rank's send buffers into
+        its neighbours' strip halo rows (one fused copy for all ranks)."""
+        H = states[0].plan.halo
+        d, x = [], []
+        for up, dn in zip(states, states[1:]):
+            su, sd = up.strips, dn.strips
+            for S_up, SB_up, S_dn, SB_dn in ((su.U, su.SU, sd.U, sd.SU),
+                                             (su.V, su.SV, sd.V, sd.SV)):
+                d += [S_dn[sd.top][0:H], S_up[su.bot][2 * H:3 * H]]
+                x += [SB_up[su.bot], SB_dn[sd.top]]
+        self._met(states, lambda: _copy_many(states[0].ops, d, x))
+        return None
+
+    @staticmethod
+    def _met(states, fn):
+        """Run fn where every virtual rank's stream has arrived, and let every
+        rank's stream continue only after it."""
+        streams = [getattr(s.ops, "stream", None) for s in states]
+        if any(x is not None for x in streams):
+            import torch
+            main = torch.cuda.current_stream(states[0].ops.device)
+            for x in streams:
+                if x is not None:
+                    main.wait_stream(x)
+            fn()
+            for x in streams:
+                if x is not None:
+                    x.wait_stream(main)
+        else:
+            fn()
+
+    def _copy_halos(self, states: Sequence["RankState"], level: int):
         p = states[0].plan
         H = p.halo
         for r in range(p.world - 1):
@@ -227,6 +282,26 @@ class DistComm:
             if r < p.world - 1:
                 ops.append(dist.P2POp(dist.isend, t(f[band.b - H:band.b]).clone(), r + 1))
                 ops.append(dist.P2POp(dist.irecv, t(f[band.b:band.b + H]), r + 1))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    def start_strips(self, states: Sequence["RankState"]):
+        """The overlapped schedule's exchange: the send buffers out, the
+        neighbours' rows straight into the strips' halo rows."""
+        import torch
+        import torch.distributed as dist
+        (s,) = states
+        p, r, H, st = s.plan, s.rank, s.plan.halo, s.strips
+        ops = []
+
+        def t(x):
+            return torch.from_numpy(x) if isinstance(x, np.ndarray) else x
+        for S, SB in ((st.U, st.SU), (st.V, st.SV)):
+            if r > 0:
+                ops.append(dist.P2POp(dist.isend, t(SB[st.top]), r - 1))
+                ops.append(dist.P2POp(dist.irecv, t(S[st.top][0:H]), r - 1))
+            if r < p.world - 1:
+                ops.append(dist.P2POp(dist.isend, t(SB[st.bot]), r + 1))
+                ops.append(dist.P2POp(dist.irecv, t(S[st.bot][2 * H:3 * H]), r + 1))
         return dist.batch_isend_irecv(ops) if ops else []
 
 
@@ -277,21 +352,34 @@ def solve(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
     return states
 
 
-def _clone(ops, x):
-    if hasattr(ops, "clone"):
-        return ops.clone(x)
-    return x if isinstance(x, tuple) else x.copy()  # numpy (oracle-backed ops)
-
-
-def _cat(ops, a, b):
-    return ops.cat_rows(a, b) if hasattr(ops, "cat_rows") else np.concatenate([a, b], 0)
-
-
-def _copy(ops, dst, src):
-    if hasattr(ops, "copy_rows"):
-        ops.copy_rows(dst, src)
+def _copy_many(ops, dsts, srcs):
+    """dst[k][...] = src[k] for every k, in stream order (DeviceOps: one
+    fused launch)"""
+    if hasattr(ops, "copy_many"):
+        ops.copy_many(dsts, srcs)
     else:
-        dst[...] = src
+        for d, x in zip(dsts, srcs):
+            d[...] = x
+
+
+def _stack(ops, planes):
+    return ops.stack(planes) if hasattr(ops, "stack") else np.stack(planes)
+
+
+def _gradients_own(ops, J0, J1):
+    """Gradients of a stack of planes [n, r, c] into storage of their own
+    (DeviceOps reuses one workspace across gradients() calls)"""
+    if hasattr(ops, "gradients_own"):
+        return ops.gradients_own(J0, J1)
+    return [ops.gradients(a, b) for a, b in zip(J0, J1)]
+
+
+def _jacobi_stack(ops, g, U, V, n: int, side=False):
+    if hasattr(ops, "jacobi_stack"):
+        ops.jacobi_stack(g, U, V, n, side)
+    else:
+        for gk, uk, vk in zip(g, U, V):
+            ops.jacobi(gk, uk, vk, n)
 
 
 def overlap_ok(p: Plan) -> bool:
@@ -300,38 +388,141 @@ def overlap_ok(p: Plan) -> bool:
     return p.world > 1 and all(bd.b - bd.a >= 2 * p.halo for lv in p.bands for bd in lv)
 
 
+class StripSet:
+    """A rank's edge strips on one level of the overlapped schedule: the
+    top strip holds rows [a - H, a + 2H), the bottom one [b - 2H, b + H),
+    planes `top` / `bot` of the [n, 3H, C] stacks U, V (views into its
+    group's stack: see strip_groups); SU, SV hold the exact rows
+    [a, a + H) / [b - H, b) a chunk produced, which the exchange sends (a
+    buffer of their own: the next chunk's snapshot rewrites the strips while
+    a send may still read them)."""
+
+    def __init__(self, s: "RankState", l: int):
+        p, H = s.plan, s.plan.halo
+        R, _ = p.sizes[l]
+        bd = p.bands[l][s.rank]
+        self.H, self.a, self.b = H, bd.a, bd.b
+        self.top = 0 if bd.a > 0 else None
+        self.bot = (1 if self.top is not None else 0) if bd.b < R else None
+        self.n = (self.top is not None) + (self.bot is not None)
+        self.rows = []
+        if self.top is not None:
+            self.rows.append((bd.a - H, bd.a + 2 * H))
+        if self.bot is not None:
+            self.rows.append((bd.b - 2 * H, bd.b + H))
+
+    def bind(self, U, V, SU, SV):
+        self.U, self.V, self.SU, self.SV = U, V, SU, SV
+
+    def snapshot(self, u, v, with_halos: bool):
+        """Owned edge rows (and, before the first chunk, the halo rows the
+        warm start left in the band) into the strips."""
+        H, a, b = self.H, self.a, self.b
+        d, x = [], []
+        for f, S in ((u, self.U), (v, self.V)):
+            if self.top is not None:
+                d.append(S[self.top][(0 if with_halos else H):3 * H])
+                x.append(f[(a - H if with_halos else a):a + 2 * H])
+            if self.bot is not None:
+                d.append(S[self.bot][0:(3 if with_halos else 2) * H])
+                x.append(f[b - 2 * H:(b + H if with_halos else b)])
+        return d, x
+
+    def write_back(self, u, v):
+        """The strips' exact middle rows into the band and the send buffers."""
+        H, a, b = self.H, self.a, self.b
+        d, x = [], []
+        for f, S, SB in ((u, self.U, self.SU), (v, self.V, self.SV)):
+            if self.top is not None:
+                d += [f[a:a + H], SB[self.top]]
+                x += [S[self.top][H:2 * H], S[self.top][H:2 * H]]
+            if self.bot is not None:
+                d += [f[b - H:b], SB[self.bot]]
+                x += [S[self.bot][H:2 * H], S[self.bot][H:2 * H]]
+        return d, x
+
+    def halos_out(self, u, v):
+        """After a level's last exchange: the received halo rows into the
+        band's halo rows (the next level's warm start reads them)."""
+        H, a, b = self.H, self.a, self.b
+        d, x = [], []
+        for f, S in ((u, self.U), (v, self.V)):
+            if self.top is not None:
+                d.append(f[a - H:a])
+                x.append(S[self.top][0:H])
+            if self.bot is not None:
+                d.append(f[b:b + H])
+                x.append(S[self.bot][2 * H:3 * H])
+        return d, x
+
+
+def _shared_stream(states) -> bool:
+    """Local ranks that run on one device stream (virtual ranks on one GPU
+    with DeviceOps(stream=None), or the oracle-backed ops)"""
+    return all(getattr(s.ops, "stream", None) is None for s in states)
+
+
+def strip_groups(states, l: int):
+    """Allocate the level's edge strips.  Local ranks on one stream share ONE
+    stack of strips (every rank's top and bottom strip, solved by one call
+    per chunk); otherwise each rank has its own.  Returns [(ops, grads, U,
+    V)], one entry per stack; sets every state's `strips`."""
+    groups = [list(states)] if _shared_stream(states) else [[s] for s in states]
+    out = []
+    for grp in groups:
+        ops = grp[0].ops
+        p, H = grp[0].plan, grp[0].plan.halo
+        C = p.sizes[l][1]
+        sets = [StripSet(s, l) for s in grp]
+        n = sum(x.n for x in sets)
+        U = _stack(ops, [ops.zeros(3 * H, C) for _ in range(n)])
+        V = _stack(ops, [ops.zeros(3 * H, C) for _ in range(n)])
+        SU = _stack(ops, [ops.zeros(H, C) for _ in range(n)])
+        SV = _stack(ops, [ops.zeros(H, C) for _ in range(n)])
+        off = 0
+        for s, x in zip(grp, sets):
+            x.bind(U[off:off + x.n], V[off:off + x.n], SU[off:off + x.n], SV[off:off + x.n])
+            s.strips = x
+            off += x.n
+        g = _gradients_own(ops, _stack(ops, [s.P0[l][r0:r1] for s in grp for r0, r1 in s.strips.rows]),
+                           _stack(ops, [s.P1[l][r0:r1] for s in grp for r0, r1 in s.strips.rows]))
+        out.append((ops, g, U, V))
+    return out
+
+
 def solve_overlapped(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
     """solve() with each chunk's halo exchange hidden behind the next
     chunk's interior iterations.  Per rank and chunk, with H = p.halo and the
     owned rows [a, b):
-      * the interior [a, b) is solved in place as its own plane: its edges at
-        a and b are artificial, so after the chunk its rows [a + H, b - H) are
-        exact -- and it needs nothing from the neighbours, so it runs (on a
-        side stream on the GPU) while the previous chunk's exchange is in
-        flight;
-      * the edge strips [a - H, a + 2H) and [b - 2H, b + H) -- the received
-        halo rows plus a snapshot of the owned rows taken before the interior
-        overwrites them -- are solved once the exchange has landed, on the
-        caller's stream, concurrently with the interior; their middle thirds
-        are the exact rows [a, a + H) and [b - H, b), written back (after
-        the interior has finished) and sent to the neighbours as copies
-        (posted, not waited for: the next interior solve may rewrite the
-        rows while a send is still reading).
-    Critical path per chunk: max(interior, exchange + strip) instead of
-    band + exchange.  Every sub-plane starts on an even image row (H and the
-    band starts are even), so every owned row is BIT-IDENTICAL to solve()
-    and to the undivided solve.  Gradients of the three sub-planes are
+      * snapshot: the owned edge rows [a, a + 2H) and [b - 2H, b) are copied
+        into the rank's edge strips (StripSet; one fused copy);
+      * the interior [a, b) is solved in place as its own plane (on a side
+        stream on the GPU): its edges at a and b are artificial, so after
+        the chunk its rows [a + H, b - H) are exact -- and it needs nothing
+        from the neighbours, so it runs while the previous chunk's exchange
+        is in flight;
+      * once that exchange has landed (the neighbours' exact rows, received
+        straight into the strips' halo rows), both strips are solved by one
+        call as a stack of two planes, concurrently with the interior; their
+        middle thirds are the exact rows [a, a + H) and [b - H, b), copied
+        (one fused copy, after the interior has finished) into the band and
+        into the send buffers, and sent to the neighbours (posted, not
+        waited for).
+    Critical path per chunk: max(interior, exchange + strips) instead of
+    band + exchange, at 4 launches per rank and chunk besides the exchange.
+    Every sub-plane starts on an even image row (H and the band starts are
+    even), so every owned row is BIT-IDENTICAL to solve() and to the
+    undivided solve.  Gradients of the interior and of the strips are
     computed once per level (their artificial edges differ from the band's)."""
     if not overlap_ok(p):
         raise ValueError("overlapped schedule needs world > 1 and bands of >= 2 halos")
-    H = p.halo
     states = [RankState(p, r, ops) for r, ops in zip(ranks, ops_list)]
     for s, I0, I1 in zip(states, I0s, I1s):
         s.P0, s.P1 = s.ops.levels(I0, I1, p.levels)
 
     for l in range(p.levels - 1, -1, -1):
         R, C = p.sizes[l]
-        g = []
+        gi = []
         for s in states:
             bd = p.bands[l][s.rank]
             s.u[l], s.v[l] = s.ops.zeros(R, C), s.ops.zeros(R, C)
@@ -340,66 +531,83 @@ def solve_overlapped(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Seque
                 c1 = min(p.sizes[l + 1][0], (bd.e1 + 1) // 2)
                 s.ops.upflow(s.u[l + 1][c0:c1], s.v[l + 1][c0:c1],
                              s.u[l][bd.e0:bd.e1], s.v[l][bd.e0:bd.e1])
-            top = bd.a > 0
-            bot = bd.b < R
-            # DeviceOps computes gradients into one reused workspace: each
-            # sub-plane keeps its own copy (which also holds its solve's
-            # ping-pong planes, so interior and strips can run concurrently)
-            gi = _clone(s.ops, s.ops.gradients(s.P0[l][bd.a:bd.b], s.P1[l][bd.a:bd.b]))
-            gt = _clone(s.ops, s.ops.gradients(s.P0[l][bd.a - H:bd.a + 2 * H],
-                                               s.P1[l][bd.a - H:bd.a + 2 * H])) if top else None
-            gb = _clone(s.ops, s.ops.gradients(s.P0[l][bd.b - 2 * H:bd.b + H],
-                                               s.P1[l][bd.b - 2 * H:bd.b + H])) if bot else None
-            g.append((gi, gt, gb, top, bot))
+            gi.append(_gradients_own(s.ops, _stack(s.ops, [s.P0[l][bd.a:bd.b]]),
+                                     _stack(s.ops, [s.P1[l][bd.a:bd.b]])))
+        groups = strip_groups(states, l)
+        shared = len(groups) == 1 and len(states) > 1
+
+        def copies(step):
+            """One fused copy for every rank of a shared stack, else per rank"""
+            if shared:
+                d, x = [], []
+                for s in states:
+                    dd, xx = step(s)
+                    d += dd
+                    x += xx
+                _copy_many(states[0].ops, d, x)
+            else:
+                for s in states:
+                    _copy_many(s.ops, *step(s))
+
         pending = None
         done = 0
         while done < iters:
             n = min(p.chunk, iters - done)
-            snaps = []
-            for s, (gi, gt, gb, top, bot) in zip(states, g):
+            first = done == 0
+            copies(lambda s: s.strips.snapshot(s.u[l], s.v[l], with_halos=first))
+            for s, g in zip(states, gi):
                 bd = p.bands[l][s.rank]
                 u, v = s.u[l], s.v[l]
-                # the owned rows the strips need, before the interior moves on
-                snaps.append((_clone(s.ops, u[bd.a:bd.a + 2 * H]) if top else None,
-                              _clone(s.ops, v[bd.a:bd.a + 2 * H]) if top else None,
-                              _clone(s.ops, u[bd.b - 2 * H:bd.b]) if bot else None,
-                              _clone(s.ops, v[bd.b - 2 * H:bd.b]) if bot else None))
                 if hasattr(s.ops, "fork"):  # interior on the side stream
                     s.ops.fork()
-                    s.ops.jacobi_side(gi, u[bd.a:bd.b], v[bd.a:bd.b], n)
-                else:
-                    s.ops.jacobi(gi, u[bd.a:bd.b], v[bd.a:bd.b], n)
+                _jacobi_stack(s.ops, g, u[None, bd.a:bd.b], v[None, bd.a:bd.b], n, side=True)
             comm.wait(pending)                                     # chunk - 1's halos
-            strips = []
-            for s, (gi, gt, gb, top, bot), (tu, tv, bu, bv) in zip(states, g, snaps):
-                bd = p.bands[l][s.rank]
-                u, v = s.u[l], s.v[l]
-                st = sb = None
-                if top:
-                    st = (_cat(s.ops, u[bd.a - H:bd.a], tu), _cat(s.ops, v[bd.a - H:bd.a], tv))
-                    s.ops.jacobi(gt, st[0], st[1], n)
-                if bot:
-                    sb = (_cat(s.ops, bu, u[bd.b:bd.b + H]), _cat(s.ops, bv, v[bd.b:bd.b + H]))
-                    s.ops.jacobi(gb, sb[0], sb[1], n)
-                strips.append((st, sb))
-            for s, (st, sb) in zip(states, strips):
-                bd = p.bands[l][s.rank]
-                u, v = s.u[l], s.v[l]
+            for ops, g, U, V in groups:
+                _jacobi_stack(ops, g, U, V, n)
+            for s in states:
                 if hasattr(s.ops, "join"):
                     s.ops.join()
-                if st is not None:
-                    _copy(s.ops, u[bd.a:bd.a + H], st[0][H:2 * H])
-                    _copy(s.ops, v[bd.a:bd.a + H], st[1][H:2 * H])
-                if sb is not None:
-                    _copy(s.ops, u[bd.b - H:bd.b], sb[0][H:2 * H])
-                    _copy(s.ops, v[bd.b - H:bd.b], sb[1][H:2 * H])
-            pending = comm.start(states, l)
+            copies(lambda s: s.strips.write_back(s.u[l], s.v[l]))
+            pending = comm.start_strips(states)
             done += n
         comm.wait(pending)
+        copies(lambda s: s.strips.halos_out(s.u[l], s.v[l]))
         for s in states:
+            s.strips = None
             if l + 1 < p.levels:
                 s.u[l + 1] = s.v[l + 1] = None
     return states
+
+
+def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
+    """Capture a whole banded solve of virtual ranks on one device (solve or
+    solve_overlapped with DeviceOps and LocalComm) into one hipGraph, so that
+    the schedule's many small stream-ordered operations (per chunk and rank:
+    band or interior and strip solves, snapshots, halo copies) cost no host
+    time.  Runs the solve eagerly once first (the library's and the ops' side
+    streams must exist before a capture).  Returns (graph, u, v): each
+    graph.replay() recomputes the level-0 (u, v) into u, v (rank 0's gather of
+    the owned rows).  DistComm's RCCL point-to-point calls are not captured:
+    N real ranks run the schedules eagerly."""
+    import torch
+    if not isinstance(comm, LocalComm):
+        raise ValueError("graphed(): LocalComm virtual ranks only")
+    if any(o.stream is not None for o in ops_list):
+        # measured: capturing the overlapped schedule with a stream per
+        # virtual rank crashes inside hipStreamEndCapture on this stack
+        raise ValueError("graphed(): virtual ranks on the caller's stream only")
+    dev = ops_list[0].device
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        gather_owned(solver(I0s, I1s, p, iters, ops_list, comm, ranks), p, comm)
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        st = solver(I0s, I1s, p, iters, ops_list, comm, ranks)
+        u, v = gather_owned(st, p, comm)
+    return g, u, v
 
 
 def gather_owned(states, p: Plan, comm):
@@ -407,6 +615,14 @@ def gather_owned(states, p: Plan, comm):
     all states are local; with DistComm every rank calls this (rank 0 gets
     the arrays, others None)."""
     if isinstance(comm, LocalComm):
+        streams = [getattr(s.ops, "stream", None) for s in states]
+        if any(x is not None for x in streams):
+            import torch
+            main = torch.cuda.current_stream(states[0].ops.device)
+            for x in streams:
+                if x is not None:
+                    main.wait_stream(x)
+
         def copy(x):
             return x.clone() if hasattr(x, "clone") else x.copy()
         u, v = copy(states[0].u[0]), copy(states[0].v[0])

@@ -30,7 +30,7 @@ def main():
     for f in glob.glob(os.path.join(d, "**", "run_kernel_trace.csv"), recursive=True):
         tr.extend(csv.DictReader(open(f)))
     ks = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]),
-                 x["Kernel_Name"].split("(")[0].replace("void ", "")) for x in tr
+                 x["Kernel_Name"].split("(")[0].replace("void ", "").split("::")[-1]) for x in tr
                 if "hs_" in x["Kernel_Name"])
     groups = []
     for k in ks:

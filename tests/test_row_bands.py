@@ -252,3 +252,36 @@ def test_device_bands_8k_fp16_eight_ranks(hs):
     I0, I1 = hs.synth_pair(1000, 4320, 7680)
     (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, 3, 5, 30, 8, 12, torch.float16)
     assert torch.equal(u, ur) and torch.equal(v, vr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlap", [False, True])
+def test_device_bands_graphed_bit_identical(hs, overlap):
+    """row_bands.graphed: the whole banded solve of virtual ranks captured
+    into one hipGraph; replays (over NaN-filled outputs) give the undivided
+    solve's bits."""
+    I0, I1 = hs.synth_pair(1000, 400, 522)
+    t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
+    p = rb.plan(400, 522, 2, 3, 5, 6)
+    ops = [rb.DeviceOps(5, 1.0, t0.device) for _ in range(3)]
+    solver = rb.solve_overlapped if overlap else rb.solve
+    g, u, v = rb.graphed(solver, [t0] * 3, [t1] * 3, p, 40, ops, rb.LocalComm(), [0, 1, 2])
+    u.fill_(float("nan"))
+    v.fill_(float("nan"))
+    g.replay()
+    g.replay()
+    ur, vr = hs.flow_pyramid_device(t0, t1, 2, 5, 40, 1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(u, ur) and torch.equal(v, vr)
+
+
+def test_graphed_refuses_dist_comm_and_rank_streams():
+    p = rb.plan(64, 30, 1, 2, 5, 2)
+
+    class O:
+        stream = object()
+        device = "cpu"
+    with pytest.raises(ValueError):
+        rb.graphed(rb.solve, [None] * 2, [None] * 2, p, 4, [O(), O()], rb.DistComm(), [0, 1])
+    with pytest.raises(ValueError):
+        rb.graphed(rb.solve, [None] * 2, [None] * 2, p, 4, [O(), O()], rb.LocalComm(), [0, 1])
