@@ -265,9 +265,19 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
 
     // one unrolled block of U time steps from row tb (even); ROWE: some
     // stage row of the block may lie outside the image (top / bottom
-    // segments)
-    auto block = [&](int tb, auto rowe_c) {
+    // segments).  FILL = f > 0: the stream's f-th block, in the pipeline
+    // fill, where stage j (0-based) receives no row it needs before its
+    // step 2 AR j (its window's first needed input): it starts there (its
+    // vertical-sum state depends on the last W arrivals alone, so the
+    // skipped steps leave no trace in any row a later stage or a store
+    // uses; identical bits).  Σ_j 2 AR j of its KB (N + KB (W - 1)) stage
+    // steps: 60 of 648 at w 5, KB 6, N 84.  (Also skipping the operator
+    // update of the next 2 AR steps, whose rows are not needed either, gave
+    // 1-ulp differences in a segment's first rows on the GPU, not kept.)
+    static_assert(2 * AR * KB == 2 * U, "the pipeline fill is two blocks");
+    auto block = [&](int tb, auto rowe_c, auto fill_c) {
         constexpr bool ROWE = decltype(rowe_c)::value;
+        constexpr int FILL = decltype(fill_c)::value;
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const int t = tb + k;
@@ -283,6 +293,9 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
 #pragma unroll
             for (int j = 0; j < KB; ++j) {
                 const int y = t - (j + 1) * AR;
+                // step within the fill (compile-time after unrolling)
+                const int kf = FILL > 0 ? (FILL - 1) * U + k : 1 << 20;
+                if (kf < 2 * AR * j) break;  // nor any later stage
                 // image-row parity of the arriving row t - j AR (tb even)
                 const int pt = (k + j * AR) & 1;
                 f2v Su, Sv;
@@ -339,12 +352,18 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // run a body without row zeroing (one body per loop: a two-body loop
     // makes the allocator spill); the rarely used variants take one loop
     // (the block's stage rows are [tb - KB AR, tb + U - 1 - AR])
+    // (every stream is at least 3 blocks: N + KB (W - 1) >= 3 U)
+    using F0 = std::integral_constant<int, 0>;
     int tb = t_first;
+    block(tb, std::true_type{}, std::integral_constant<int, 1>{});
+    tb += U;
+    block(tb, std::true_type{}, std::integral_constant<int, 2>{});
+    tb += U;
     if constexpr (X2 && !G32) {
-        for (; tb <= t_last && tb - KB * AR < 0; tb += U) block(tb, std::true_type{});
-        for (; tb <= t_last && tb + U - 1 - AR < rows; tb += U) block(tb, std::false_type{});
+        for (; tb <= t_last && tb - KB * AR < 0; tb += U) block(tb, std::true_type{}, F0{});
+        for (; tb <= t_last && tb + U - 1 - AR < rows; tb += U) block(tb, std::false_type{}, F0{});
     }
-    for (; tb <= t_last; tb += U) block(tb, std::true_type{});
+    for (; tb <= t_last; tb += U) block(tb, std::true_type{}, F0{});
 }
 
 // ---------------------------------------------------------------- kernel
