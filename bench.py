@@ -86,6 +86,12 @@ PARITY_TOL = 1e-4          # north_star: 1e-4 relative (norm form)
 GOLDEN_JSON = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 GOLDEN_NPZ = os.path.join(ROOT, "tests", "golden", "bench_golden.npz")
 PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r03.json")
+KERNEL_SOURCES = ("hsflow_strips.hip", "hsflow_kernels.hip", "hsflow_device.h")
+# measured VALU issue cost per wave64 instruction per SIMD (shader cycles)
+# at each Jacobi kernel's occupancy: profiles/r02_valu_tput.txt, mean of
+# v_add / v_add_dpp / v_pk_add / v_fma / v_pk_fma at 2 (K4) and 4 (K2)
+# waves per SIMD
+ISSUE_CYCLES = {"hs_jacobi_strip_kernel": 4.84, "hs_jacobi_wg_kernel": 3.32}
 # HSFLOW_* variables the bench itself reads (rehearsal of the N > 1 logic
 # with several ranks on one GPU); every other HSFLOW_* name is refused
 BENCH_ENV = {"HSFLOW_BENCH_BACKEND", "HSFLOW_BENCH_DEVICE"}
@@ -269,16 +275,28 @@ def pmc_key(wl_name, window, batch):
     return f"{wl_name}_w{window}_b{batch}"
 
 
+def kernel_source_md5():
+    """md5 of the Jacobi kernels' sources: a committed PMC profile is used
+    only for the kernel code it was collected on"""
+    import hashlib
+    h = hashlib.md5()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "cpp-optical-flow_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def pmc_for(wl_name, window, batch, kb, kernel):
     """Committed PMC summary of this roofline launch (profiles/pmc_r03.json,
     written by scripts/pmc_r03.py from separate rocprofv3 --pmc passes of
-    this same command) if it was collected for this kernel, blocking depth
-    and batch."""
+    the same launches) if it was collected for this kernel, blocking depth,
+    batch and kernel source."""
     if not os.path.exists(PMC_JSON):
         return None
     with open(PMC_JSON) as f:
         e = json.load(f).get(pmc_key(wl_name, window, batch))
-    if e and e.get("kb") == kb and e.get("kernel") == kernel:
+    if e and e.get("kb") == kb and e.get("kernel") == kernel and \
+            e.get("kernel_source_md5") == kernel_source_md5():
         return e
     return None
 
@@ -328,7 +346,7 @@ def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
             "algorithmic_B_per_px_pass": PASS_BYTES_PER_PX,
             "naive_equiv_frac": round(naive / HBM_PEAK_GBPS, 4),
             "naive_B_per_px_iter": NAIVE_BYTES_PER_PX_ITER,
-            "hbm_frac": None, "valu_frac": None}
+            "hbm_frac": None, "valu_frac": None, "valu_issue_frac": None}
     pmc = pmc_for(wl_name, window, batch, kb, kernel)
     if pmc is not None and pmc.get("hbm_bytes_per_launch"):
         traffic = pmc["hbm_bytes_per_launch"]
@@ -344,6 +362,11 @@ def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
             # shader cycles (GRBM_GUI_ACTIVE / 8 XCDs)
             roof["valu_frac"] = round(pmc["valu_insts_per_launch"] * 2.0 / 1024 /
                                       pmc["launch_cycles"], 4)
+            if kernel in ISSUE_CYCLES:
+                # the same at the issue rate the kernel's occupancy allows
+                roof["valu_issue_frac"] = round(
+                    pmc["valu_insts_per_launch"] * ISSUE_CYCLES[kernel] / 1024 /
+                    pmc["launch_cycles"], 4)
             roof["clock_ghz"] = pmc.get("clock_ghz")
         roof["pmc_source"] = pmc.get("source")
     del u, v

@@ -110,8 +110,15 @@ def leg_summary(ldir, calib):
     return e
 
 
+def kernel_source_md5():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.kernel_source_md5()
+
+
 def main():
     d = sys.argv[1]
+    md5 = kernel_source_md5()
     calib = calibration(d)
     with open(os.path.join(ROOT, "profiles", "pmc_r03_calib.json"), "w") as f:
         json.dump({"bytes_per_dispatch": CALIB_BYTES, "source": "scripts/ubench/fetch_calib.hip",
@@ -121,6 +128,7 @@ def main():
         if os.path.isdir(ldir) and os.path.basename(ldir) != "calib":
             e = leg_summary(ldir, calib)
             if e:
+                e["kernel_source_md5"] = md5
                 out[os.path.basename(ldir)] = e
     with open(os.path.join(ROOT, "profiles", "pmc_r03.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)

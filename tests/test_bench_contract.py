@@ -139,3 +139,21 @@ def test_gpus_mismatch_with_launcher_refuses():
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 2 and "WORLD_SIZE=1" in out.stderr
     assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_pmc_profile_used_only_for_the_kernel_source_it_was_collected_on(tmp_path, monkeypatch):
+    """bench.pmc_for: a committed counter profile feeds roofline.traffic only
+    when kernel, blocking depth and the kernels' source md5 all match."""
+    import json
+    import bench
+    md5 = bench.kernel_source_md5()
+    e = {"kernel": "hs_jacobi_strip_kernel", "kb": 6, "hbm_bytes_per_launch": 1,
+         "kernel_source_md5": md5}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"1080p_w5_b8": e}))
+    monkeypatch.setattr(bench, "PMC_JSON", str(p))
+    assert bench.pmc_for("1080p", 5, 8, 6, "hs_jacobi_strip_kernel") == e
+    assert bench.pmc_for("1080p", 5, 8, 8, "hs_jacobi_strip_kernel") is None
+    assert bench.pmc_for("1080p", 5, 8, 6, "hs_jacobi_wg_kernel") is None
+    p.write_text(json.dumps({"1080p_w5_b8": dict(e, kernel_source_md5="0" * 32)}))
+    assert bench.pmc_for("1080p", 5, 8, 6, "hs_jacobi_strip_kernel") is None
