@@ -439,6 +439,12 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
         return n;
     };
     int best_n = aligned(override_rows > 0 ? override_rows : 84);
+    // w = 5 (KB 6): 84-row segments measured best on every shape that runs
+    // K4 once the pipeline fill is skipped (same box, N 48..240: 1080p x 8,
+    // 4K x 1 and x 2, and 8K, where the model below would take 168 rows and
+    // one round of waves: 1.13 M against 1.14-1.15 M Mpix*iter/s at 84,
+    // alternated on one box)
+    if (override_rows <= 0 && W == 5 && KB == 6) override_rows = best_n;
     if (override_rows <= 0) {
         const long simds = slots / 2 > 0 ? slots / 2 : 1;
         double best = -1.0;
