@@ -11,8 +11,10 @@ tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
     > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
+t0=$SECONDS
 timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err \
     || { echo "bench rc=$?"; tail -20 gpurun_out/bench_default.err; cat gpurun_out/bench_default.json; exit 1; }
+echo "bench wall seconds: $((SECONDS - t0))" | tee gpurun_out/bench_wall.txt
 cat gpurun_out/bench_default.json
 [ "$1" = "--trace" ] || exit 0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/bench_trace -o run --output-format csv -- \
