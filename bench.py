@@ -149,9 +149,10 @@ def parse(argv=None):
 
 # --------------------------------------------------------------- guards
 def refuse_diagnostics(environ=None):
-    """Names of HSFLOW_* variables that could change the measured work
-    (diagnostic switches live only in the probe build, but the bench refuses
-    them outright so a stray variable can never produce a number)."""
+    """Names of HSFLOW_* variables set in the environment other than the
+    bench's own.  The library reads none, but hsflow.py honours HSFLOW_LIB
+    (another build of the library, for same-box A/B): the bench refuses them
+    all so a stray variable can never produce a number."""
     environ = os.environ if environ is None else environ
     return sorted(k for k in environ if k.startswith("HSFLOW_") and k not in BENCH_ENV)
 
@@ -761,9 +762,9 @@ def main():
     import torch.distributed as dist
     import hsflow
 
-    if hsflow.is_probe_build():
-        print(f"bench: {hsflow.LIB_PATH} is the probe build; rebuild the product library",
-              file=sys.stderr)
+    if hsflow.is_probe_build():  # hsflow_build_flags() != 0: not the product build
+        print(f"bench: {hsflow.LIB_PATH} was built with development flags; rebuild the "
+              "product library", file=sys.stderr)
         sys.exit(2)
     # HSFLOW_BENCH_BACKEND=gloo + HSFLOW_BENCH_DEVICE=0: rehearse the N > 1
     # logic with several ranks on one GPU (diagnostics; the driver's runs
