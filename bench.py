@@ -777,10 +777,15 @@ def main():
 
     def init_dist():
         if world > 1 and not state["up"]:
+            # a collective that never completes (a mismatched RCCL
+            # send/recv order, a dead peer) aborts the run after 5 minutes
+            # instead of holding the node; every leg takes well under that
+            import datetime
+            limit = datetime.timedelta(minutes=5)
             if backend == "nccl":
-                dist.init_process_group("nccl", device_id=dev)
+                dist.init_process_group("nccl", device_id=dev, timeout=limit)
             else:
-                dist.init_process_group(backend)
+                dist.init_process_group(backend, timeout=limit)
             state["up"] = True
 
     if args.mode == "stream":
