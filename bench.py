@@ -101,8 +101,8 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="GPUs = ranks; without a launcher bench.py starts them itself")
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p")
     ap.add_argument("--batch", type=int, default=0, help="pairs per GPU per step")
     ap.add_argument("--iters", type=int, default=0)
@@ -248,13 +248,47 @@ def parity_check(u, v, golden):
 
 
 # --------------------------------------------------------------- timing
-def timed_region(step, sync, steps, warmup, world, device):
+PREWARM_S = 0.15
+
+
+def prewarm(step, sync, seconds=PREWARM_S, max_steps=400):
+    """Untimed steps until `seconds` of load have passed, before the W
+    warm-up steps: the GPU needs ~0.1 s under load to reach its steady
+    clocks (same box, 1080p x 8: 2 warm-up steps read 1.22-1.24 M, 20 read
+    1.33 M, 60 1.34 M), so a short driver warm-up would time
+    the clock ramp, not the kernels.  Returns (steps, seconds) run."""
+    sync()
+    t0 = time.perf_counter()
+    n = 0
+    while n < max_steps:
+        step()
+        n += 1
+        if n % 4 == 0 or n == 1:
+            sync()
+            if time.perf_counter() - t0 >= seconds:
+                break
+    sync()
+    return n, time.perf_counter() - t0
+
+
+def timed_region(step, sync, steps, warmup, world, device, info=None, prewarm_s=0.0,
+                 before_timing=None):
     """The driver's timing rule: W untimed steps, barrier + sync, K timed
-    steps, sync; the slowest rank's time."""
+    steps, sync; the slowest rank's time.  With prewarm_s > 0, `prewarm`
+    runs first (untimed; what it ran goes into `info`) -- only for steps
+    without collectives: a time-bounded loop may run different step counts
+    on different ranks."""
     import torch
     import torch.distributed as dist
+    if prewarm_s > 0:
+        n, t = prewarm(step, sync, prewarm_s)
+        if info is not None:
+            info["prewarm_steps"] = n
+            info["prewarm_s"] = round(t, 3)
     for _ in range(warmup):
         step()
+    if before_timing is not None:
+        before_timing()
     sync()
     if world > 1:
         dist.barrier()
@@ -443,17 +477,22 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, window=None, b
         else:
             solve(stream)
 
-    # the output planes hold NaN when the timed steps start: the parity
-    # check below passes only if the replays themselves wrote (u, v)
-    u.fill_(float("nan"))
-    v.fill_(float("nan"))
+    # the output planes hold NaN when the timed steps start (filled after
+    # the pre-warm and warm-up replays): the parity check below passes only
+    # if the timed replays themselves wrote (u, v)
+    def nan_fill():
+        u.fill_(float("nan"))
+        v.fill_(float("nan"))
+    nan_fill()
     torch.cuda.synchronize(dev)
     # the process group comes up after the first capture: no communicator
     # thread touches the device while a stream is capturing
     if init_dist is not None:
         init_dist()
+    warm = {}
     elapsed = timed_region(step, lambda: torch.cuda.synchronize(dev), args.steps,
-                           args.warmup, world, dev)
+                           args.warmup, world, dev, info=warm, prewarm_s=PREWARM_S,
+                           before_timing=nan_fill)
 
     # parity of the timed output: pair 0 of rank 0 is seed 1000
     parity = None
@@ -483,7 +522,7 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, window=None, b
            "value": round(value, 1), "unit": "Mpix*iter/s",
            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
            "pairs_per_s_resident": round(total_pairs / elapsed, 2),
-           "step": step_kind, "roofline": roof, "parity": parity}
+           "step": step_kind, "untimed_prewarm": warm, "roofline": roof, "parity": parity}
     del I0, I1, ws, pws
     torch.cuda.empty_cache()
     if keep:
@@ -886,6 +925,7 @@ def main():
                                             "levels", "input_dtype", "alpha",
                                             "pairs_per_gpu_per_step", "step")},
             "pairs_per_s_resident": prim["pairs_per_s_resident"],
+            "untimed_prewarm": prim["untimed_prewarm"],
             "parity": prim["parity"],
             "roofline": prim["roofline"],
             "cpu_baseline": cpu,
