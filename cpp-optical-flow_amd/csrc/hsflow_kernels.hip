@@ -976,12 +976,21 @@ int device_cus() {
     return cus;
 }
 
-// workgroups of a workgroup-kernel launch with RW-row slabs (8 waves)
-static long wg_tiles(const JacobiArgs &a, int W, int KB, int RW) {
+// workgroups of a workgroup-kernel launch with RW-row slabs (NW waves)
+static long wg_tiles(const JacobiArgs &a, int W, int KB, int RW, int NW = 8) {
     const int HL = KB * (W - W / 2 - 1), HR = KB * (W / 2);
     const int ox = 128 - (HL + (HL & 1)) - (HR + (HR & 1));
-    const int oy = 8 * RW - KB * (W - 1);
+    const int oy = NW * RW - KB * (W - 1);
     return (long)((a.cols + ox - 1) / ox) * ((a.rows + oy - 1) / oy) * a.batch;
+}
+
+// Slab rows the busiest SIMD sweeps per iteration: workgroups per CU (the
+// launch spread evenly) x waves per SIMD of one workgroup x slab rows.  A
+// launch that cannot fill the chip ends when its busiest SIMD does.
+static long wg_simd_rows(const JacobiArgs &a, int W, int KB, int RW, int NW) {
+    const long cus = device_cus();
+    const long per_cu = (wg_tiles(a, W, KB, RW, NW) + cus - 1) / cus;
+    return per_cu * (NW / 4) * RW;
 }
 
 // Blocking depth for a launch that does not fill the chip.  KB = 6 is the
@@ -1042,6 +1051,18 @@ static hipError_t launch_jacobi_wgv(JacobiArgs a, hipStream_t s) {
     // spill).  Used for w = 5 and w = 6 (8 -> 10 rows: 1080p 782 k -> 859 k,
     // 4K 793 k -> 891 k); at w = 3 and w = 4 they measure equal to the
     // all-register slabs.
+    // Fill-limited KB 8 launches (a single 1080p pair: 460 8-wave tiles for
+    // 512 slots, so two workgroups, 40 slab rows, on the busiest SIMD):
+    // 16-wave workgroups of 8-row slabs (128-row regions, one per CU: 128 KB
+    // of exchange buffers) cover 1080p in 240 tiles, 32 rows per SIMD.  Taken
+    // when the busiest SIMD sweeps fewer rows that way.  Same box, one pair,
+    // 300 it: 1080p w 5 0.825 -> 0.790 ms, w 3 0.717 -> 0.700 ms, bit-identical;
+    // 720p x 2 and KITTI keep the 8-wave tiles (scripts/lab/geom_ab.sh,
+    // profiles/r03_k2_geometry_ab.txt).
+    if constexpr ((W == 3 || W == 5) && KB == 8) {
+        if (wg_simd_rows(a, W, KB, 8, 16) < wg_simd_rows(a, W, KB, wg_rows(W), 8))
+            return launch_jacobi_wg<W, KB, 8, 16, 16>(a, s);
+    }
     constexpr int RT = (W == 5 || W == 6) ? wg_rows_tl(W) : 0;
     if constexpr (RT > 0 && KB * (W - 1) < 8 * RT / 2) {
         bool on = true;

@@ -262,6 +262,22 @@ def test_batch_equals_single_pairs(hs, ctx):
         assert norm_rel_err(u[i].cpu().numpy(), uo) <= TOL
 
 
+@pytest.mark.parametrize("w", [3, 5])
+def test_single_pair_geometry_equals_batch(hs, w):
+    """A single 1080p pair runs K2 at depth 8 in 16-wave x 8-row tiles (the
+    fill-limited geometry); the same pair inside a batch of two runs other
+    tiles and depths (K4 / 8-wave K2): the same bits."""
+    import torch
+    pairs = [hs.synth_pair(1000 + i, 1080, 1920) for i in range(2)]
+    b0 = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    b1 = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    assert hs.iters_per_launch(1080, 1920, 1, w) == 8
+    u, v = hs.flow_device(b0, b1, w, 40, 1.0)
+    us, vs = hs.flow_device(b0[0].contiguous(), b1[0].contiguous(), w, 40, 1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(u[0], us) and torch.equal(v[0], vs)
+
+
 def test_warm_start_continuation_is_exact(hs):
     import torch
     I0, I1 = hs.synth_pair(3, 240, 320)
