@@ -318,6 +318,7 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
     a.gy = w.gy;
     a.gt = w.gt;
     a.flags = w.flags;
+    a.write_through = hsflow::fill_limited(window, kb, strip, rows, cols, fill_batch) ? 1 : 0;
     // pass p writes the caller's buffers iff (passes-1-p) is even, so the
     // last pass always lands in (u, v)
     auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };

@@ -19,6 +19,8 @@ struct JacobiArgs {
     const float *gx, *gy, *gt; // f32 gradients (non-integral inputs)
     const uint32_t *flags;     // per pair: 0 -> gpack valid, else f32 planes
     int seg_rows;              // K4 strip kernel: output rows per segment
+    int write_through;         // store u', v' write-through (sc1) instead of nt: launches
+                               // that do not fill the chip (fill_limited)
 };
 
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
@@ -46,5 +48,8 @@ int default_kb(int W);
 // default_kb adjusted for launches that do not fill one round of slots
 int fill_kb(int W, int kb, int rows, int cols, int batch);
 bool kb_supported(int W, int KB, bool need_f32);
+// the solve's launches leave most of the chip idle (all pairs in flight):
+// their outputs are stored write-through (JacobiArgs::write_through)
+bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch);
 
 }  // namespace hsflow

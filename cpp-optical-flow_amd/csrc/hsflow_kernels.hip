@@ -643,24 +643,34 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     const auto vo_rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0,
                                                          nbytes, 0x00020000);
     const bool st_lane = lane >= HLc / 2 && lane < (HLc + OX) / 2;
-    // u', v' are streamed out with the nt policy: +0.7 % at 1080p x 8, +-0 at
-    // 4K x 2 against default-policy stores (same box; sc0 stores +0.2 %)
-    constexpr int SAUX = 2;
+    // u', v' are streamed out with the nt policy in launches that fill the
+    // chip (+0.7 % at 1080p x 8, +-0 at 4K x 2 against default-policy stores;
+    // sc0 +0.2 %; sc1 -4 % / -2 %) and write-through (sc1) in the others
+    // (p.write_through: a single 1080p pair +9 %, 720p x 2 +4 %, KITTI +3 %;
+    // profiles/r03_store_policy_ab.txt) -- their lines leave the L2 at once
+    // instead of at the kernel boundary.  A wave-uniform branch per row.
     auto store_row = [&](int r, int vo_e, int vo_o) {
         const int wr = wv * RW + r;  // workgroup region row (wave-uniform)
         if (!(wr >= HL && wr < HL + OY && ((rowmask >> r) & 1ull))) return;
         const int so = (r0 + r) * cols * 4;
-        if constexpr (X2) {
-            __builtin_amdgcn_raw_buffer_store_b64(
-                u2v{__float_as_uint(U[r].x), __float_as_uint(U[r].y)}, uo_rs, vo_e, so, SAUX);
-            __builtin_amdgcn_raw_buffer_store_b64(
-                u2v{__float_as_uint(V[r].x), __float_as_uint(V[r].y)}, vo_rs, vo_e, so, SAUX);
-        } else {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].x), uo_rs, vo_e, so, SAUX);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].y), uo_rs, vo_o, so, SAUX);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].x), vo_rs, vo_e, so, SAUX);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, vo_o, so, SAUX);
-        }
+        auto st = [&](auto aux_c) {
+            constexpr int AUX = decltype(aux_c)::value;
+            if constexpr (X2) {
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    u2v{__float_as_uint(U[r].x), __float_as_uint(U[r].y)}, uo_rs, vo_e, so, AUX);
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    u2v{__float_as_uint(V[r].x), __float_as_uint(V[r].y)}, vo_rs, vo_e, so, AUX);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].x), uo_rs, vo_e, so, AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(U[r].y), uo_rs, vo_o, so, AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].x), vo_rs, vo_e, so, AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(V[r].y), vo_rs, vo_o, so, AUX);
+            }
+        };
+        if (p.write_through)
+            st(std::integral_constant<int, 16>{});
+        else
+            st(std::integral_constant<int, 2>{});
     };
     auto iteration = [&](int it, auto last_c) {
         constexpr bool LAST = decltype(last_c)::value;
@@ -1013,6 +1023,22 @@ int fill_kb(int W, int kb, int rows, int cols, int batch) {
     if (wg_tiles(a, 5, 6, wg_rows_tl(5)) >= slots) return kb;
     const long t8 = std::max(wg_tiles(a, 5, 8, wg_rows_tl(5)), wg_tiles(a, 5, 8, wg_rows(5)));
     return t8 <= slots ? 8 : kb;
+}
+
+bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch) {
+    if (rows <= 0 || cols <= 0 || batch <= 0) return false;
+    JacobiArgs a{};
+    a.rows = rows;
+    a.cols = cols;
+    a.batch = batch;
+    if (strip) {  // K4: under 3/4 of the wave slots (a 4K pair: 962 of 2048)
+        int nseg = 0, nstrips = 0;
+        strip_seg_rows(W, KB, rows, cols, batch, 1, &nseg, &nstrips, 84);
+        return (long)nseg * nstrips * batch * 4 < 8L * device_cus() * 3;
+    }
+    // K2: one round of 8-wave tiles (a single 1080p pair: 460 for 512 slots)
+    if (W < 3 || W > 9) return false;
+    return wg_tiles(a, W, KB, wg_rows(W)) <= 2L * device_cus();
 }
 
 template <int W, int KB, int RW, int NW, int SB>

@@ -185,7 +185,7 @@ __device__ __forceinline__ void hrow(f2v u, f2v v, f2v &hu, f2v &hv) {
 // Segment body: rows [a, b) of strip columns [c0, c0 + 128) of one pair,
 // streamed downwards.  U = unroll period (multiple of the operator ring
 // KB*AR, of 2 and of D).
-template <int W, int KB, int D, int U, bool X2, bool G32>
+template <int W, int KB, int D, int U, bool X2, bool G32, bool WT>
 __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, int plane_bytes,
                                            int c0, int a, int b) {
     constexpr int A = W - W / 2 - 1, AR = W / 2;
@@ -325,21 +325,31 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                     const bool sin = y >= a && y < b;
                     const int so = sin ? y * row_bytes : (int)0x80000000;
                     const int oe = st_e;
-                    if constexpr (X2) {
-                        __builtin_amdgcn_raw_buffer_store_b64(
-                            u2v{__float_as_uint(nu.x), __float_as_uint(nu.y)}, rs.uo, oe, so, 2);
-                        __builtin_amdgcn_raw_buffer_store_b64(
-                            u2v{__float_as_uint(nv.x), __float_as_uint(nv.y)}, rs.vo, oe, so, 2);
-                    } else {
-                        const int oo = st_o;
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.x), rs.uo, oe, so,
-                                                              2);
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.y), rs.uo, oo, so,
-                                                              2);
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.x), rs.vo, oe, so,
-                                                              2);
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.y), rs.vo, oo, so,
-                                                              2);
+                    // nt, or write-through (sc1) in launches that leave most
+                    // of the chip idle (WT, from p.write_through: a 4K pair
+                    // +8.5 %; 4K x 2 -2 %, 1080p x 8 -4 % with sc1).  A
+                    // template parameter: a run-time branch here cost the
+                    // full-chip launches 3 % (profiles/r03_store_policy_ab.txt)
+                    {
+                        constexpr int AUX = WT ? 16 : 2;
+                        if constexpr (X2) {
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                u2v{__float_as_uint(nu.x), __float_as_uint(nu.y)}, rs.uo, oe, so,
+                                AUX);
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                u2v{__float_as_uint(nv.x), __float_as_uint(nv.y)}, rs.vo, oe, so,
+                                AUX);
+                        } else {
+                            const int oo = st_o;
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.x), rs.uo, oe,
+                                                                  so, AUX);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nu.y), rs.uo, oo,
+                                                                  so, AUX);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.x), rs.vo, oe,
+                                                                  so, AUX);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv.y), rs.vo, oo,
+                                                                  so, AUX);
+                        }
                     }
                 }
             }
@@ -372,7 +382,7 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
 // (strips fastest), so the strips that share halo columns run side by side;
 // the XCD-aware remap gives each XCD a contiguous run of them (its L2
 // serves the shared halo columns and the rows two segments both read).
-template <int W, int KB, int D, int U>
+template <int W, int KB, int D, int U, bool WT>
 __global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs p) {
     const int nblk = gridDim.x;
     const int lin = blockIdx.x;
@@ -395,14 +405,14 @@ __global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
     if (g32) {
         if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, true>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, true, true, WT>(p, pbase, plane_bytes, c0, a, b);
         else
-            strip_body<W, KB, D, U, false, true>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, false, true, WT>(p, pbase, plane_bytes, c0, a, b);
     } else {
         if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, false>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, true, false, WT>(p, pbase, plane_bytes, c0, a, b);
         else
-            strip_body<W, KB, D, U, false, false>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, false, false, WT>(p, pbase, plane_bytes, c0, a, b);
     }
 }
 
@@ -491,12 +501,23 @@ hipError_t launch_jacobi_strip(JacobiArgs a, int W, int KB, int seg_rows, hipStr
     const long waves = (long)nstrips * nseg * a.batch;
     if (waves <= 0 || waves > 0x7FFFFFFFL) return hipErrorInvalidValue;
     dim3 grd((unsigned)waves, 1, 1);
+    const bool wt = a.write_through != 0;
     if (W == 5 && KB == 6) {
         using C = StripCfg<5, 6>;
-        hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U>), grd, dim3(64), 0, s, a);
+        if (wt)
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U, true>), grd, dim3(64), 0,
+                               s, a);
+        else
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U, false>), grd, dim3(64), 0,
+                               s, a);
     } else if (W == 3 && KB == 8) {
         using C = StripCfg<3, 8>;
-        hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U>), grd, dim3(64), 0, s, a);
+        if (wt)
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U, true>), grd, dim3(64), 0,
+                               s, a);
+        else
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U, false>), grd, dim3(64), 0,
+                               s, a);
     } else {
         return hipErrorInvalidValue;
     }

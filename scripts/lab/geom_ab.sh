@@ -1,9 +1,10 @@
 #!/bin/bash
 # A/B of lab builds (cpp-optical-flow_amd/lab/libhsflow_TAG.so), alternated,
 # then a bitwise comparison of their u planes.  bash scripts/lab/geom_ab.sh A B
+# (SHAPES=tag,tag,... limits the shapes)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/geom
 for r in 1 2; do for t in "$@"; do
-  timeout -k 5 180 python -u scripts/lab/geom_probe.py $t gpurun_out/geom || exit 1
+  timeout -k 5 240 python -u scripts/lab/geom_probe.py $t gpurun_out/geom $SHAPES || exit 1
 done; done
 python3 - "$@" <<'PY'
 import sys, glob, numpy as np

@@ -15,10 +15,13 @@ import torch
 
 SHAPES = [("1080p_w5", 1080, 1920, 5, 300, 1), ("1080p_w3", 1080, 1920, 3, 300, 1),
           ("720p_x2", 720, 1280, 5, 300, 2), ("kitti", 375, 1242, 5, 100, 1),
-          ("4k", 2160, 3840, 5, 500, 1)]
+          ("4k", 2160, 3840, 5, 500, 1), ("1080p_x8", 1080, 1920, 5, 300, 8),
+          ("4k_x2", 2160, 3840, 5, 500, 2)]
+if len(sys.argv) > 3:  # a subset: comma-separated tags
+    SHAPES = [s for s in SHAPES if s[0] in sys.argv[3].split(",")]
 
 
-def timed(I0, I1, w, iters, reps=30):
+def timed(I0, I1, w, iters, reps=20):
     rows, cols = I0.shape[-2:]
     b = I0.shape[0]
     ws = hsflow.alloc_workspace(rows, cols, b)
