@@ -1,7 +1,7 @@
 """Per-workgroup timeline of one K2 pass of a single 1080p pair (lab build
 with s_memrealtime stamps, 100 MHz): kernel start, slab loaded + operator
 set up, first iteration done, last iteration's stores issued, stores drained.
-python scripts/lab/stamp_probe.py [w]"""
+python scripts/lab/stamp_probe.py [w] [lab tag]"""
 import ctypes
 import json
 import os
@@ -12,7 +12,8 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
 sys.path.insert(0, os.path.join(ROOT, "cpp-optical-flow_amd"))
 import numpy as np
 import hsflow
-hsflow.LIB_PATH = os.path.join(ROOT, "cpp-optical-flow_amd", "lab", "libhsflow_stamp.so")
+hsflow.LIB_PATH = os.path.join(ROOT, "cpp-optical-flow_amd", "lab",
+                               f"libhsflow_{sys.argv[2] if len(sys.argv) > 2 else 'stamp'}.so")
 import torch
 
 w = int(sys.argv[1]) if len(sys.argv) > 1 else 5
@@ -45,3 +46,16 @@ for iters in (8, 16):
                   "drain_us": q(rel[:, 4] - rel[:, 3]),
                   "end_us": q(rel[:, 4])}
     print(iters, json.dumps(res[iters]), flush=True)
+    if iters == 16:  # per tile: where are the slow ones?
+        info = buf[np.any(buf != 0, axis=1)][:, 5].astype(np.int64)
+        info = info[st[:, 0] > 0] if len(info) == len(st) else info
+        tx, ty = info & 0xFFFF, (info >> 16) & 0xFFFF
+        edge, rowe = (info >> 32) & 1, (info >> 33) & 1
+        end = rel[:, 4]
+        it = rel[:, 3] - rel[:, 2]
+        for name, m in (("interior", edge == 0), ("edge_cols", (edge == 1) & (rowe == 0)),
+                        ("edge_rows", (edge == 1) & (rowe == 1))):
+            if m.any():
+                print(" ", name, int(m.sum()), "rest_iters", q(it[m]), "end", q(end[m]), flush=True)
+        slow = np.argsort(-end)[:8]
+        print("  slowest", [(int(tx[i]), int(ty[i]), round(float(end[i]), 2)) for i in slow], flush=True)
