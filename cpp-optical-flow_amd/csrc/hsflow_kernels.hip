@@ -380,6 +380,30 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                                           float2 *tpl, int tx, int ty, int wv, int lane,
                                           size_t pbase, int plane_bytes);
 
+// A wave whose slab lies wholly outside the image: its rows are u = v = 0
+// in every iteration (BORDER_CONSTANT), so it publishes zero boundary sums
+// once (both exchange buffers) and then only takes the workgroup's barriers
+// -- the same sequence as wg_body_p's iterations (one per iteration, and a
+// second after each but the last when the exchange is single-buffered).
+// It stores nothing: no row of it is in the image.
+template <int W, int RW, int NW>
+__device__ __forceinline__ void wg_zero_wave(const JacobiArgs &p,
+                                             float2 (&xch)[wg_nbuf(W, RW)][NW][W - 1][2][64],
+                                             int wv, int lane) {
+#pragma unroll
+    for (int b = 0; b < wg_nbuf(W, RW); ++b)
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k) {
+            xch[b][wv][k][0][lane] = make_float2(0.f, 0.f);
+            xch[b][wv][k][1][lane] = make_float2(0.f, 0.f);
+        }
+    const int n_it = p.iters;
+    for (int it = 0; it < n_it; ++it) {
+        __syncthreads();
+        if (wg_nbuf(W, RW) == 1 && it + 1 < n_it) __syncthreads();
+    }
+}
+
 // One wave's slab, specialised on the parity of its first image row (the
 // order of the vertical sums follows image-row parity, see wg_body_p): a
 // whole body per parity, so no register state lives across the two.
@@ -463,8 +487,20 @@ __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
     // widths take per-column dword accesses.  Pairs K1 flagged as
     // non-integral read the f32 gradient planes instead of the packed words
     // (same tiles, same operator, any blocking depth).
-    const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols &&
-                          ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows;
+    //
+    // The body is chosen per wave (all take the same barriers): a wave whose
+    // slab lies wholly outside the image only publishes zeros (its rows are
+    // u = v = 0 every iteration); a wave wholly inside needs no row zeroing
+    // (the per-row selects cost a whole tile row 18 % at 1080p, where every
+    // slab is wholly inside or outside); only a slab that straddles the
+    // top or bottom edge runs the row-zeroing body.
+    const int r0w = ty * OY - HL + wv * RW;  // image row of this wave's slab row 0
+    if (r0w + RW <= 0 || r0w >= p.rows) {
+        wg_zero_wave<W, RW, NW>(p, xch, wv, lane);
+        return;
+    }
+    const bool w_in = r0w >= 0 && r0w + RW <= p.rows;
+    const bool interior = tx * OX - HLc >= 0 && tx * OX - HLc + RX <= cols && w_in;
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
     if (g32) {
         if ((cols & 1) == 0)
@@ -479,8 +515,8 @@ __device__ __forceinline__ void wg_tile(const JacobiArgs &p,
         if (interior)
             wg_body<W, KB, RW, NW, SB, false, true, false>(p, xch, tpl, tx, ty, wv, lane, pbase,
                                                            plane_bytes);
-        else if (W <= 7 && ty * OY - HL >= 0 && ty * OY - HL + RY <= p.rows)
-            // left/right border tiles: every region row inside the image
+        else if (W <= 7 && w_in)
+            // left/right border tiles: every slab row inside the image
             wg_body<W, KB, RW, NW, SB, true, true, false, false>(p, xch, tpl, tx, ty, wv,
                                                                  lane, pbase, plane_bytes);
         else
