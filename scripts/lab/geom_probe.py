@@ -17,7 +17,8 @@ SHAPES = [("1080p_w5", 1080, 1920, 5, 300, 1), ("1080p_w3", 1080, 1920, 3, 300, 
           ("720p_x2", 720, 1280, 5, 300, 2), ("kitti", 375, 1242, 5, 100, 1),
           ("4k", 2160, 3840, 5, 500, 1), ("1080p_x8", 1080, 1920, 5, 300, 8),
           ("4k_x2", 2160, 3840, 5, 500, 2)]
-if len(sys.argv) > 3:  # a subset: comma-separated tags
+ALL = list(SHAPES)
+if len(sys.argv) > 3 and sys.argv[3]:  # a subset: comma-separated tags
     SHAPES = [s for s in SHAPES if s[0] in sys.argv[3].split(",")]
 
 
@@ -52,6 +53,8 @@ def timed(I0, I1, w, iters, reps=20):
 
 out = {}
 os.makedirs(sys.argv[2], exist_ok=True)
+if len(sys.argv) > 4:  # an explicit order, repeats allowed
+    SHAPES = [next(s for s in ALL if s[0] == t) for t in sys.argv[4].split(",")]
 for tag, rows, cols, w, iters, b in SHAPES:
     ps = [hsflow.synth_pair(1000 + i, rows, cols) for i in range(b)]
     I0 = torch.from_numpy(np.stack([p[0] for p in ps])).cuda()
