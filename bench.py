@@ -30,14 +30,22 @@ timed replays themselves computed (u, v); a parity miss anywhere exits 3.
                 pairs: pair 0 vs the golden, pairs 0..7 bit for bit against
                 the resident solve of the same seeds), [4] (8K fp16, 3 levels
                 x 1000 it)
-  roofline      dominant kernel (K2, the Jacobi pass) measured live with
-                events on its launch stream.  achieved = the algorithmic
+  roofline      the dominant kernel, the Jacobi pass (`kernel`: K4
+                hs_jacobi_strip_kernel or K2 hs_jacobi_wg_kernel, whichever
+                the library runs for the leg).  The top-level figures
+                describe the TIMED step: avg_launch_ms = ms_per_step / passes
+                per solve (the wall time of one pass of the whole batch, both
+                side streams, K1's share included -- so the kernel's time per
+                step never exceeds ms_per_step); achieved = the algorithmic
                 bytes of one temporally blocked pass (read u, v and the
                 packed gradients, write u, v: 20 B per pixel; the first pass
-                reads no u, v) / launch time, frac = achieved / 8 TB/s
-                (a physical fraction, <= 1); traffic / hbm_frac = PMC bytes
-                per launch (committed profile of this command,
-                profiles/pmc_r03.json) / launch time / 8 TB/s;
+                reads no u, v) / avg_launch_ms, frac = achieved / 8 TB/s (a
+                physical fraction, <= 1); traffic = PMC bytes per pass of the
+                timed configuration (profiles/pmc_r04.json, rocprofv3 --pmc of
+                scripts/timed_step.py), hbm_frac = traffic / avg_launch_ms /
+                8 TB/s.  `isolated_launch`: one single-stream launch timed
+                with events on its stream (what rocprofv3 reports per
+                dispatch), with its own PMC bytes and VALU issue fractions;
                 naive_equiv_frac = SURVEY §8(d)'s 28 B per pixel-iteration x
                 the iterations one launch performs / launch time / 8 TB/s
                 (the rate a one-iteration-per-launch kernel would need;
@@ -53,8 +61,17 @@ timed replays themselves computed (u, v); a parity miss anywhere exits 3.
                 of (u, v) f32, copies overlapped with solves on other streams
   stream        BASELINE config 4: 64 pairs held by rank 0, scattered over
                 RCCL (point-to-point), solved, (u, v) gathered back, checked
+  bands         BASELINE config 5 as stated for N GPUs: ONE 8K fp16 pair
+                (3 levels x 1000 it) split into N row bands with a halo
+                exchange over RCCL (row_bands.solve), checked against the
+                8k_w5_l3 golden; at N = 1 one band (the config5 leg's solve
+                through the band machinery)
+  host_api      the reference's own call (main.cpp:97-98): one pair through
+                hsflow_flow from pageable host u8 frames to CV_64FC1 (u, v)
+                (hornSchunck.cpp:49-50, 72-73), 1080p and 4K, with parity
   cpu_baseline  the float64 CPU port (oracle/, mirrors hornSchunck.cpp pass
-                by pass) on a bounded sample, 1 thread, rank 0 only
+                by pass) on a bounded sample, 1 thread, rank 0 (also on N > 1
+                lines: the host-core figure next to every GPU count)
 """
 from __future__ import annotations
 
@@ -85,7 +102,7 @@ NAIVE_BYTES_PER_PX_ITER = 28  # f32 u, v, Ix, Iy, It in, u', v' o
 PARITY_TOL = 1e-4          # north_star: 1e-4 relative (norm form)
 GOLDEN_JSON = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 GOLDEN_NPZ = os.path.join(ROOT, "tests", "golden", "bench_golden.npz")
-PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r03.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r04.json")
 KERNEL_SOURCES = ("hsflow_strips.hip", "hsflow_kernels.hip", "hsflow_device.h")
 # measured VALU issue cost per wave64 instruction per SIMD (shader cycles)
 # at each Jacobi kernel's occupancy: profiles/r02_valu_tput.txt, mean of
@@ -130,6 +147,10 @@ def parse(argv=None):
                     help="skip the single-pair blocks of the default run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pairs/s leg")
     ap.add_argument("--no-stream", action="store_true", help="skip the config-4 stream leg")
+    ap.add_argument("--no-bands", action="store_true",
+                    help="skip the config-5 row-band leg of the default run")
+    ap.add_argument("--no-host-api", action="store_true",
+                    help="skip the host-buffer getFlow leg of the default run")
     ap.add_argument("--mode", choices=["resident", "stream", "bands"], default="resident",
                     help="resident: pairs generated on each rank, already in HBM "
                          "(the metric, plus the secondary / e2e / stream legs); stream: "
@@ -321,15 +342,17 @@ def kernel_source_md5():
     return h.hexdigest()
 
 
-def pmc_for(wl_name, window, batch, kb, kernel):
-    """Committed PMC summary of this roofline launch (profiles/pmc_r03.json,
-    written by scripts/pmc_r03.py from separate rocprofv3 --pmc passes of
-    the same launches) if it was collected for this kernel, blocking depth,
-    batch and kernel source."""
+def pmc_for(wl_name, window, batch, kb, kernel, timed=False):
+    """Committed PMC summary of this roofline leg (profiles/pmc_r04.json,
+    written by scripts/pmc_collect.py from separate rocprofv3 --pmc passes)
+    if it was collected for this kernel, blocking depth, batch and kernel
+    source.  timed: the timed configuration's entry (scripts/timed_step.py:
+    the bench's graph-replayed solve on its side streams) instead of the
+    single-stream launches."""
     if not os.path.exists(PMC_JSON):
         return None
     with open(PMC_JSON) as f:
-        e = json.load(f).get(pmc_key(wl_name, window, batch))
+        e = json.load(f).get(("step_" if timed else "") + pmc_key(wl_name, window, batch))
     if e and e.get("kb") == kb and e.get("kernel") == kernel and \
             e.get("kernel_source_md5") == kernel_source_md5():
         return e
@@ -337,11 +360,13 @@ def pmc_for(wl_name, window, batch, kb, kernel):
 
 
 def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters, alpha,
-                 reps, step_s=None, ws=None):
-    """The dominant kernel alone (the Jacobi pass, K2), single stream, timed
-    with events on its launch stream: the per-launch duration rocprofv3
-    reports per dispatch.  Config 5: the level-0 plane, the pass that
-    dominates its solve."""
+                 reps, step_ms=None, ws=None):
+    """Roofline of the dominant kernel, the Jacobi pass (K4 or K2, as the
+    library picks for the leg).  Top level: the TIMED step (step_ms =
+    ms_per_step of the leg): one pass of the whole batch takes step_ms /
+    passes of wall time.  `isolated_launch`: one single-stream launch timed
+    with events on its stream -- the per-dispatch duration rocprofv3
+    reports.  Config 5: the level-0 plane, the pass that dominates its solve."""
     import torch
     kb = hsflow.iters_per_launch(rows, cols, batch, window)
     kernel = hsflow.jacobi_kernel_name(rows, cols, batch, window)
@@ -373,37 +398,63 @@ def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
     pass_bytes = n_px * (PASS_BYTES_PER_PX - 8 / launches_per_solve)
     achieved = pass_bytes / (k2_ms * 1e-3) / 1e9
     naive = NAIVE_BYTES_PER_PX_ITER * n_px * iters / launches_per_solve / (k2_ms * 1e-3) / 1e9
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-            "kernel": kernel, "avg_launch_ms": round(k2_ms, 5),
-            "iters_per_launch": kb, "launches_per_solve": launches_per_solve,
-            "algorithmic_bytes_per_launch": int(pass_bytes),
-            "algorithmic_B_per_px_pass": PASS_BYTES_PER_PX,
-            "naive_equiv_frac": round(naive / HBM_PEAK_GBPS, 4),
-            "naive_B_per_px_iter": NAIVE_BYTES_PER_PX_ITER,
-            "hbm_frac": None, "valu_frac": None, "valu_issue_frac": None}
+    iso = {"avg_launch_ms": round(k2_ms, 5), "achieved": round(achieved, 1),
+           "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+           "naive_equiv_frac": round(naive / HBM_PEAK_GBPS, 4),
+           "naive_B_per_px_iter": NAIVE_BYTES_PER_PX_ITER,
+           "hbm_frac": None, "valu_frac": None, "valu_issue_frac": None,
+           "timing": "single stream, events on the launch stream"}
     pmc = pmc_for(wl_name, window, batch, kb, kernel)
     if pmc is not None and pmc.get("hbm_bytes_per_launch"):
         traffic = pmc["hbm_bytes_per_launch"]
-        roof["traffic"] = traffic
-        roof["traffic_over_algorithmic"] = round(traffic / pass_bytes, 3)
+        iso["traffic"] = traffic
+        iso["traffic_over_algorithmic"] = round(traffic / pass_bytes, 3)
         # physical HBM utilisation: the PMC bytes at the live launch time
-        roof["hbm_frac"] = round(traffic / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-        roof["hbm_frac_vs_copy_peak"] = round(
+        iso["hbm_frac"] = round(traffic / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        iso["hbm_frac_vs_copy_peak"] = round(
             traffic / (k2_ms * 1e-3) / 1e9 / COPY_PEAK_GBPS, 4)
         if pmc.get("valu_insts_per_launch") and pmc.get("launch_cycles"):
             # VALU issue at the guide's 2 cycles per wave64 instruction per
             # SIMD (MI355X_MICROARCH.md constants table) over the launch's
             # shader cycles (GRBM_GUI_ACTIVE / 8 XCDs)
-            roof["valu_frac"] = round(pmc["valu_insts_per_launch"] * 2.0 / 1024 /
-                                      pmc["launch_cycles"], 4)
+            iso["valu_frac"] = round(pmc["valu_insts_per_launch"] * 2.0 / 1024 /
+                                     pmc["launch_cycles"], 4)
             if kernel in ISSUE_CYCLES:
                 # the same at the issue rate the kernel's occupancy allows
-                roof["valu_issue_frac"] = round(
+                iso["valu_issue_frac"] = round(
                     pmc["valu_insts_per_launch"] * ISSUE_CYCLES[kernel] / 1024 /
                     pmc["launch_cycles"], 4)
-            roof["clock_ghz"] = pmc.get("clock_ghz")
-        roof["pmc_source"] = pmc.get("source")
+            iso["clock_ghz"] = pmc.get("clock_ghz")
+        iso["pmc_source"] = pmc.get("source")
+    # the timed step: one pass of the whole batch per step_ms / passes
+    pass_ms = step_ms / launches_per_solve if step_ms else k2_ms
+    ach = pass_bytes / (pass_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": kernel, "avg_launch_ms": round(pass_ms, 5),
+            "timing": ("timed step: ms_per_step / passes per solve (hipGraph replay, "
+                       "batch split over the side streams; K1 included)") if step_ms
+                      else "isolated launch",
+            "iters_per_launch": kb, "launches_per_solve": launches_per_solve,
+            "algorithmic_bytes_per_launch": int(pass_bytes),
+            "algorithmic_B_per_px_pass": PASS_BYTES_PER_PX, "hbm_frac": None,
+            "naive_equiv_frac": round(NAIVE_BYTES_PER_PX_ITER * n_px * iters /
+                                      launches_per_solve / (pass_ms * 1e-3) / 1e9 /
+                                      HBM_PEAK_GBPS, 4),
+            "isolated_launch": iso}
+    tp = pmc_for(wl_name, window, batch, kb, kernel, timed=True) if step_ms else None
+    if tp is not None and tp.get("hbm_bytes_per_step"):
+        per_pass = tp["hbm_bytes_per_step"] / launches_per_solve
+        roof["traffic"] = int(per_pass)
+        roof["traffic_over_algorithmic"] = round(per_pass / pass_bytes, 3)
+        roof["hbm_frac"] = round(per_pass / (pass_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        roof["traffic_source"] = tp.get("source")
+    elif iso["traffic"] is not None:
+        # no profile of the timed configuration: the isolated launch's bytes
+        roof["traffic"] = iso["traffic"]
+        roof["traffic_over_algorithmic"] = iso["traffic_over_algorithmic"]
+        roof["hbm_frac"] = round(iso["traffic"] / (pass_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        roof["traffic_source"] = "isolated launch PMC bytes (" + str(iso.get("pmc_source")) + ")"
     del u, v
     return roof
 
@@ -511,8 +562,11 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, window=None, b
     del u, v, graph
     roof = None
     if roofline:
+        # config 5: the level-0 plane's passes are most of the step, not all
         roof = roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
-                            alpha, args.roofline_reps, ws=ws if levels == 1 else None)
+                            alpha, args.roofline_reps,
+                            step_ms=elapsed / args.steps * 1e3 if levels == 1 else None,
+                            ws=ws if levels == 1 else None)
 
     leg = {"workload": f"{wl_name} {cols}x{rows}, {iters} it"
                        + (f"/level x {levels} levels" if levels > 1 else "")
@@ -885,10 +939,19 @@ def main():
         golden = golden_entry(1080, 1920, 300, 5, 1, 1.0) if rank == 0 else None
         strm = stream_leg("1080p", args, world, rank, dev, ref=resident_ref, golden=golden)
     del resident_ref
+    bands = None
+    if default_run and not args.no_bands:
+        # BASELINE configs[4] as stated for N GPUs: one 8K pair in N row
+        # bands, halo rows over RCCL (at N = 1: one band, no exchange)
+        init_dist()
+        bands = bands_leg(args, world, rank, dev, steps=max(1, min(args.steps, 5)), warmup=1)
 
     c1 = config1_leg(dev) if (default_run and rank == 0) else None
+    host_api = host_api_leg() if (default_run and rank == 0 and not args.no_host_api) else None
     cpu = cpu_all = None
-    if rank == 0 and not args.no_cpu_baseline and world == 1:
+    if rank == 0 and not args.no_cpu_baseline:
+        # on every line, N > 1 included: the host-core figure the GPU counts
+        # are read against (north_star)
         cpu = cpu_baseline(prim["rows"], prim["cols"], args.window, args.alpha,
                            args.cpu_iters)
         # SURVEY §8(d) second CPU line: all cores of the box's CPU share
@@ -896,6 +959,7 @@ def main():
         n_thr = min(16, os.cpu_count() or 1)
         cpu_all = cpu_baseline(prim["rows"], prim["cols"], args.window, args.alpha,
                                args.cpu_iters, n_thr)
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
         if sec is not None:
             # the CPU line per config -- 4K on 1 thread, bounded
             sec["cpu_baseline"] = cpu_baseline(sec["rows"], sec["cols"], args.window,
@@ -953,10 +1017,16 @@ def main():
             line["torch_copy_gbps"] = stream_peak
         if strm is not None:
             line["stream"] = strm
+        if bands is not None:
+            line["bands"] = bands
+        if host_api is not None:
+            line["host_api"] = host_api
         # one verdict per BASELINE config
-        legs = {"configs[0]": [c1], "configs[1]": [prim, singles.get("1080p"), w3],
-                "configs[2]": [sec, singles.get("4k")], "configs[3]": [strm],
-                "configs[4]": [c5]}
+        ha = host_api or {}
+        legs = {"configs[0]": [c1], "configs[1]": [prim, singles.get("1080p"), w3,
+                                                    ha.get("1080p")],
+                "configs[2]": [sec, singles.get("4k"), ha.get("4k")], "configs[3]": [strm],
+                "configs[4]": [c5, bands]}
         verdict = {}
         for name, ls in legs.items():
             ps = [l["parity"] for l in ls if l is not None and l.get("parity") is not None]
@@ -965,7 +1035,7 @@ def main():
         line["parity_all"] = {"ok": all(v is not False for v in verdict.values()),
                               "configs": verdict}
         print(json.dumps(line), flush=True)
-        for leg in (prim, sec, w3, c5, c1, strm, *singles.values()):
+        for leg in (prim, sec, w3, c5, c1, strm, bands, *singles.values(), *ha.values()):
             if leg is not None and leg.get("parity") is not None and \
                     leg["parity"].get("ok") is False:
                 print(f"bench: PARITY FAILURE on {leg.get('workload', 'stream')}: "
@@ -977,13 +1047,20 @@ def main():
         sys.exit(status)
 
 
-def bands_mode(args, world, rank, dev):
-    """BASELINE config 5 across ranks: one pair (default the 8k workload,
-    fp16, 3 levels) split into row bands; every `--chunk` iterations each
-    rank exchanges halo rows with its neighbours over RCCL, and rank 0
+def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, ops=None,
+              result=None):
+    """BASELINE config 5 across ranks: one pair (the 8k workload, fp16, 3
+    levels, 1000 it/level unless the flags say otherwise) split into row
+    bands; every `chunk` iterations each rank exchanges halo rows with its
+    neighbours (RCCL point-to-point under the nccl backend), and rank 0
     gathers (u, v).  Timed: pyramid build + banded levels + exchanges +
     gather (inputs broadcast from rank 0 beforehand, resident in HBM).
-    Strong scaling: the work is fixed, value = pair Mpix*iter/s."""
+    Strong scaling: the work is fixed.  Rank 0's dict carries the parity of
+    the gathered (u, v) against the 8k_w5_l3 golden (bit-identical to the
+    single-GPU solve by construction, row_bands.py).  `ops` replaces the
+    libhsflow band operations (tests/test_bench_ranks.py runs this leg over
+    gloo with the CPU oracle as the band solver); a `result` list receives
+    rank 0's gathered (u, v)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -995,6 +1072,8 @@ def bands_mode(args, world, rank, dev):
     iters = args.iters or wl["iters"]
     levels = args.levels or wl.get("levels", 1)
     in_dtype = args.dtype or wl.get("dtype", "f32")
+    window, alpha = args.window, args.alpha
+    chunk = chunk or args.chunk
     tdt = {"f16": torch.float16, "f32": torch.float32, "u8": torch.uint8}[in_dtype]
     I0 = torch.empty((rows, cols), dtype=tdt, device=dev)
     I1 = torch.empty_like(I0)
@@ -1006,44 +1085,114 @@ def bands_mode(args, world, rank, dev):
     if world > 1:
         dist.broadcast(I0, 0)
         dist.broadcast(I1, 0)
-    p = rb.plan(rows, cols, levels, world, args.window, args.chunk)
-    ops = [rb.DeviceOps(args.window, args.alpha, dev)]
+    p = rb.plan(rows, cols, levels, world, window, chunk)
+    ops = [ops if ops is not None else rb.DeviceOps(window, alpha, dev)]
     comm = rb.DistComm() if world > 1 else rb.LocalComm()
     res = [None]
 
-    overlap = bool(args.overlap) and rb.overlap_ok(p)
+    overlap = bool(args.overlap if overlap is None else overlap) and rb.overlap_ok(p)
     solve = rb.solve_overlapped if overlap else rb.solve
 
     def one():
         states = solve([I0], [I1], p, iters, ops, comm, [rank])
         res[0] = rb.gather_owned(states, p, comm)
 
-    elapsed = timed_region(one, lambda: torch.cuda.synchronize(dev), args.steps, args.warmup,
-                           world, dev)
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    elapsed = timed_region(one, sync, steps, warmup, world, dev)
     px_all = sum(r * c for r, c in p.sizes)
+    exchanges = sum(-(-iters // chunk) for _ in range(levels)) if world > 1 else 0
+    leg = {"workload": f"{cols}x{rows} {in_dtype}, {levels} levels, {iters} it/level, "
+                       f"ws {window}, one pair in {world} row band" + ("s" if world > 1 else ""),
+           "value": round(px_all * iters * steps / elapsed / 1e6, 1), "unit": "Mpix*iter/s",
+           "ms_per_pair": round(elapsed / steps * 1e3, 3), "steps": steps,
+           "pairs_per_s": round(steps / elapsed, 2),
+           "n_ranks": world, "chunk": chunk, "halo_rows": p.halo,
+           "exchanges_per_solve": exchanges,
+           "exchange": "overlapped with interior iterations" if overlap else "after every chunk",
+           "transport": _transport(world, dev), "scaling": "strong"}
+    if rank == 0:
+        u, v = (np.asarray(x.cpu().numpy() if hasattr(x, "cpu") else x) for x in res[0])
+        golden = golden_entry(rows, cols, iters, window, levels, alpha)
+        leg["parity"] = parity_check(u, v, golden)
+        if result is not None:
+            result.append((u, v))
+    del I0, I1, res
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    return leg
+
+
+def bands_mode(args, world, rank, dev):
+    """--mode bands: the bands leg alone, its own JSON line."""
+    import torch.distributed as dist
+    leg = bands_leg(args, world, rank, dev, args.steps, args.warmup)
     status = 0
     if rank == 0:
-        u, v = res[0]
-        golden = golden_entry(rows, cols, iters, args.window, levels, args.alpha)
-        parity = parity_check(u.cpu().numpy(), v.cpu().numpy(), golden)
         print(json.dumps({
             "metric": "Mpix*iter/s (config 5: one pair in row bands, halo exchange over RCCL)",
-            "value": round(px_all * iters * args.steps / elapsed / 1e6, 1),
-            "unit": "Mpix*iter/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "value": leg["value"], "unit": "Mpix*iter/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": leg["ms_per_pair"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "f32", "data": f"synthetic {in_dtype} frame pair",
-            "config": {"workload": f"{cols}x{rows}, {levels} levels, {iters} it/level",
-                       "window": args.window, "chunk": args.chunk, "halo_rows": p.halo,
-                       "exchange": "overlapped with interior iterations" if overlap
-                       else "after every chunk",
+            "dtype": "f32", "data": "synthetic frame pair",
+            "config": {"workload": leg["workload"], "window": args.window,
+                       "chunk": leg["chunk"], "halo_rows": leg["halo_rows"],
+                       "exchange": leg["exchange"],
                        "parallelism": f"row bands x{world}"},
-            "parity": parity}), flush=True)
-        status = 3 if parity.get("ok") is False else 0
+            "parity": leg["parity"], "bands": leg}), flush=True)
+        status = 3 if leg["parity"].get("ok") is False else 0
     if world > 1:
         dist.destroy_process_group()
     if status:
         sys.exit(status)
+
+
+def host_api_leg(reps=15):
+    """The reference's own call as a drop-in sees it (main.cpp:97-98;
+    hornSchunck.cpp:43-75): ONE pair of pageable host u8 gray frames through
+    hsflow_flow (upload, K1, the Jacobi passes, download) to float64
+    (CV_64FC1) u, v, blocking.  Outputs reused across calls as
+    cv::Mat::create() keeps them (the adapter's steady state in a frame
+    loop); the first-touch cost of fresh output pages is reported beside it,
+    as is f32 output.  Median of `reps`; parity of the f64 output against
+    the committed golden (u, v) of seed 1000."""
+    import numpy as np
+    import hsflow
+    out = {}
+    for wl in ("1080p", "4k"):
+        w = WORKLOADS[wl]
+        rows, cols, iters = w["rows"], w["cols"], w["iters"]
+        I0, I1 = hsflow.synth_pair(1000, rows, cols, dtype=np.uint8)
+        hs = hsflow.hornSchunck(5, iters, 1.0)
+        u = np.empty((rows, cols), np.float64)
+        v = np.empty((rows, cols), np.float64)
+        hs.getFlow(I0, I1, u, v)  # warm: contexts, buffers, pool threads
+
+        def med(fn, n=reps):
+            ts = []
+            for _ in range(n):
+                t = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t)
+            return sorted(ts)[len(ts) // 2] * 1e3
+
+        u.fill(np.nan)
+        v.fill(np.nan)
+        ms = med(lambda: hs.getFlow(I0, I1, u, v))
+        par = parity_check(u, v, golden_entry(rows, cols, iters, 5, 1, 1.0))
+        ms_fresh = med(lambda: hs.getFlow(I0, I1), max(3, reps // 3))
+        ctx = hs._c()
+        u32 = np.empty((rows, cols), np.float32)
+        v32 = np.empty((rows, cols), np.float32)
+        ms_f32 = med(lambda: ctx.flow(I0, I1, 5, iters, 1.0, out_dtype=np.float32,
+                                      out=(u32, v32)), max(3, reps // 3))
+        out[wl] = {"workload": f"{cols}x{rows} u8 pair, ws 5, alpha 1, {iters} it",
+                   "ms_per_call": round(ms, 3),
+                   "Mpix_iter_per_s": round(rows * cols * iters / ms / 1e3, 1),
+                   "output": "CV_64FC1 (float64), buffers reused (cv::Mat::create)",
+                   "ms_per_call_fresh_outputs": round(ms_fresh, 3),
+                   "ms_per_call_f32_outputs": round(ms_f32, 3),
+                   "parity": par}
+    return out
 
 
 def cpu_baseline(rows, cols, window, alpha, cpu_iters, threads=1):

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -34,11 +35,11 @@ struct hsflow_ctx {
     size_t d_out_bytes = 0;  // holds u, v (or gx, gy, gt)
     void *d_ws = nullptr;
     size_t d_ws_bytes = 0;
-    // pinned host staging for the f32 results
-    float *h_stage = nullptr;
+    // pinned host staging: [uploaded frames][downloaded f32 planes]
+    char *h_stage = nullptr;
     size_t h_stage_bytes = 0;
-    // one event per staged plane of a download (created on first use)
-    hipEvent_t dl_ev[3] = {nullptr, nullptr, nullptr};
+    // one event per downloaded row chunk (created on first use)
+    std::vector<hipEvent_t> dl_ev;
 };
 
 namespace {
@@ -318,7 +319,8 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
     a.gy = w.gy;
     a.gt = w.gt;
     a.flags = w.flags;
-    a.write_through = hsflow::fill_limited(window, kb, strip, rows, cols, fill_batch) ? 1 : 0;
+    a.write_through =
+        hsflow::fill_limited(window, kb, strip, rows, cols, fill_batch, strip_rows) ? 1 : 0;
     // pass p writes the caller's buffers iff (passes-1-p) is even, so the
     // last pass always lands in (u, v)
     auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };
@@ -343,7 +345,14 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
         a.v_out = dst_is_user(pass) ? v : w.v2;
         // a K2 pass (a shorter last pass of a K4 solve) takes a depth K2 is
         // built for: any depth >= its iterations gives the same bits
-        const int kb2 = hsflow::kb_supported(window, kb, maybe_f32) ? kb : a.iters;
+        int kb2 = kb;
+        if (!hsflow::kb_supported(window, kb2, maybe_f32)) {
+            kb2 = a.iters;
+            while (kb2 < 8 && !hsflow::kb_supported(window, kb2, maybe_f32)) ++kb2;
+            if (!hsflow::kb_supported(window, kb2, maybe_f32))
+                return fail(ctx, HSFLOW_ERR_ARG, "no K2 depth >= %d for window %d", a.iters,
+                            window);
+        }
         hipError_t e = (strip && a.iters == kb)
                            ? hsflow::launch_jacobi_strip(a, window, kb, strip_rows, s)
                            : hsflow::launch_jacobi(a, window, kb2, s);
@@ -446,73 +455,36 @@ int grow_host(hsflow_ctx *ctx, size_t need) {
     return HSFLOW_OK;
 }
 
-// Host rows (any supported dtype, any step) -> dense device rows of the
-// same type (K1 takes the Sobel sums of CV_64FC1 frames in float64, as
-// hornSchunck.cpp:23-28 do, and rounds each gradient to f32 once).
-int upload(hsflow_ctx *ctx, const void *src, int dtype, int rows, int cols, size_t step,
-           void *dst, int *dev_dtype) {
-    const size_t es = (size_t)elem_size(dtype);
-    HIP_TRY(ctx, hipMemcpy2DAsync(dst, cols * es, src, step, cols * es, rows,
-                                  hipMemcpyHostToDevice, ctx->stream));
-    *dev_dtype = dtype;
+// Pinned stage layout of a host-buffer call: the uploaded frames first, the
+// downloaded planes after them (both used within one call, which ends with
+// the stream drained).
+size_t stage_bytes(size_t up_bytes, int n_down, size_t plane_px) {
+    return align_up(up_bytes) + (size_t)n_down * plane_px * 4;
+}
+
+// Two host frames (any supported dtype, any row steps) -> dense device rows
+// of the same type, through the pinned stage in row chunks
+// (hsflow_hostio.cpp; K1 takes the Sobel sums of CV_64FC1 frames in float64,
+// as hornSchunck.cpp:23-28 do, and rounds each gradient to f32 once).
+int upload_pair(hsflow_ctx *ctx, const void *I0, const void *I1, int elem, int rows, int cols,
+                size_t step0, size_t step1, void *dst0, void *dst1) {
+    const void *src[2] = {I0, I1};
+    const size_t step[2] = {step0, step1};
+    void *dst[2] = {dst0, dst1};
+    HIP_TRY(ctx, hsflow::upload_frames(src, step, 2, rows, cols, elem, dst, ctx->h_stage,
+                                       ctx->stream));
     return HSFLOW_OK;
 }
 
-// f32 stage rows -> f64 host rows (the caller's CV_64FC1 buffer), split
-// over a few host threads: the writes first-touch the caller's freshly
-// allocated pages, which dominates a single-threaded conversion
-void widen_rows(const float *stage, int rows, int cols, void *dst, size_t step) {
-    auto run = [&](int r0, int r1) {
-        for (int r = r0; r < r1; ++r) {
-            double *d = (double *)((char *)dst + (size_t)r * step);
-            const float *s = stage + (size_t)r * cols;
-            for (int c = 0; c < cols; ++c) d[c] = (double)s[c];
-        }
-    };
-    const size_t px = (size_t)rows * cols;
-    unsigned hw = std::thread::hardware_concurrency();
-    int nt = (int)std::min<unsigned>(8u, hw ? hw : 1u);
-    if (px < (1u << 18) || nt <= 1 || rows < 2 * nt) {
-        run(0, rows);
-        return;
-    }
-    std::vector<std::thread> pool;
-    const int per = (rows + nt - 1) / nt;
-    for (int t = 1; t < nt; ++t) {
-        const int r0 = t * per, r1 = std::min(rows, r0 + per);
-        if (r0 < r1) pool.emplace_back(run, r0, r1);
-    }
-    run(0, std::min(rows, per));
-    for (auto &th : pool) th.join();
-}
-
-// n dense device f32 planes -> host rows of dtype_out with step `step`.
-// f64: every plane's copy is queued into its own stage slot at once, and
-// plane k is widened while planes k+1.. are still in flight.
+// n dense device f32 planes -> host rows of dtype_out with step `step`: row
+// chunks downloaded by DMA into the stage behind the uploaded frames and
+// widened (or copied) by the host pool as they arrive.
 int download_planes(hsflow_ctx *ctx, const float *const *src, void *const *dst, int n,
-                    int rows, int cols, int dtype_out, size_t step) {
-    if (dtype_out == HSFLOW_F32) {
-        for (int k = 0; k < n; ++k)
-            HIP_TRY(ctx, hipMemcpy2DAsync(dst[k], step, src[k], (size_t)cols * 4,
-                                          (size_t)cols * 4, rows, hipMemcpyDeviceToHost,
-                                          ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        return HSFLOW_OK;
-    }
-    const size_t plane = (size_t)rows * cols;
-    int rc = grow_host(ctx, plane * 4 * n);
-    if (rc) return rc;
-    for (int k = 0; k < n; ++k) {
-        if (!ctx->dl_ev[k])
-            HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->dl_ev[k], hipEventDisableTiming));
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_stage + k * plane, src[k], plane * 4,
-                                    hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipEventRecord(ctx->dl_ev[k], ctx->stream));
-    }
-    for (int k = 0; k < n; ++k) {
-        HIP_TRY(ctx, hipEventSynchronize(ctx->dl_ev[k]));
-        widen_rows(ctx->h_stage + k * plane, rows, cols, dst[k], step);
-    }
+                    int rows, int cols, int dtype_out, size_t step, size_t up_bytes) {
+    float *stage = (float *)(ctx->h_stage + align_up(up_bytes));
+    HIP_TRY(ctx, hsflow::download_planes_pipelined(src, dst, n, rows, cols,
+                                                   dtype_out == HSFLOW_F64, step, stage,
+                                                   ctx->dl_ev, ctx->stream));
     return HSFLOW_OK;
 }
 
@@ -628,6 +600,31 @@ int pyramid_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, 
     return HSFLOW_OK;
 }
 
+// hsflow_flow_multi's kept contexts: one per (device, slot), each behind its
+// own lock (calls that list disjoint devices run concurrently); the registry
+// lock only guards the table's shape.  Slots are never freed (stable
+// pointers); hsflow_flow_multi_release destroys their contexts.
+struct MultiSlot {
+    std::mutex mu;
+    hsflow_ctx *ctx = nullptr;
+};
+std::mutex g_multi_mu;
+std::vector<std::vector<std::unique_ptr<MultiSlot>>> g_multi;  // [device][slot]
+
+std::vector<MultiSlot *> multi_slots(const int *devices, int nw) {
+    std::lock_guard<std::mutex> reg(g_multi_mu);
+    std::vector<MultiSlot *> out(nw);
+    for (int k = 0; k < nw; ++k) {
+        int dup = 0;  // earlier workers on the same device
+        for (int i = 0; i < k; ++i) dup += devices[i] == devices[k];
+        if ((int)g_multi.size() <= devices[k]) g_multi.resize(devices[k] + 1);
+        auto &dv = g_multi[devices[k]];
+        while ((int)dv.size() <= dup) dv.push_back(std::make_unique<MultiSlot>());
+        out[k] = dv[dup].get();
+    }
+    return out;
+}
+
 }  // namespace
 
 extern "C" {
@@ -683,8 +680,7 @@ void hsflow_destroy(hsflow_ctx *ctx) {
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-    for (hipEvent_t e : ctx->dl_ev)
-        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->dl_ev) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -789,9 +785,11 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, wsb))) return rc;
     char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
     float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
-    int dt0 = 0, dt1 = 0;
-    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step0, in0, &dt0))) return rc;
-    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step1, in1, &dt1))) return rc;
+    const size_t up_bytes = 2 * n * in_es;
+    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 2, n)))) return rc;
+    if ((rc = upload_pair(ctx, I0, I1, (int)in_es, rows, cols, in_step0, in_step1, in0, in1)))
+        return rc;
+    const int dt0 = dtype_in;
     rc = gradients_impl(ctx, in0, in1, dt0, rows, cols, 1, nullptr, nullptr, nullptr,
                         ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
@@ -801,7 +799,7 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     {
         const float *srcs[2] = {du, dv};
         void *dsts[2] = {u, v};
-        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step, up_bytes)))
             return rc;
     }
     return HSFLOW_OK;
@@ -830,42 +828,33 @@ int hsflow_flow_multi(const int *devices, int n_devices, int batch,
         if (devices[k] < 0 || devices[k] >= ndev)
             return fail(nullptr, HSFLOW_ERR_NODEV, "device %d of %d", devices[k], ndev);
     const int nw = std::min(n_devices, batch);
-    // Contexts (device buffers, pinned stage, stream) are kept across calls,
-    // one per (device, slot): a caller that sends frame after frame through
-    // here pays no allocation or device synchronisation per call.  One
-    // multi call at a time owns them.
-    static std::mutex mu;
-    static std::vector<std::vector<hsflow_ctx *>> ctx_pool;  // [device][slot]
-    std::lock_guard<std::mutex> lock(mu);
-    if ((int)ctx_pool.size() < ndev) ctx_pool.resize(ndev);
-    std::vector<hsflow_ctx **> slot(nw);
-    for (int k = 0; k < nw; ++k) {
-        int dup = 0;  // earlier workers on the same device
-        for (int i = 0; i < k; ++i) dup += devices[i] == devices[k];
-        auto &dv = ctx_pool[devices[k]];
-        if ((int)dv.size() <= dup) dv.resize(dup + 1, nullptr);
-        slot[k] = &dv[dup];
-    }
+    std::vector<MultiSlot *> slot = multi_slots(devices, nw);
     std::vector<int> rc(nw, HSFLOW_OK);
     std::vector<std::string> msg(nw);
     std::vector<std::thread> pool;
     pool.reserve(nw);
     for (int k = 0; k < nw; ++k) {
         pool.emplace_back([&, k] {
+            std::lock_guard<std::mutex> hold(slot[k]->mu);
             int r = HSFLOW_OK;
-            if (!*slot[k]) {
-                r = hsflow_create(slot[k], devices[k]);
+            if (!slot[k]->ctx) {
+                r = hsflow_create(&slot[k]->ctx, devices[k]);
                 if (r) {
                     rc[k] = r;
                     msg[k] = hsflow_last_error(nullptr);  // this worker's message
                     return;
                 }
             }
-            hsflow_ctx *ctx = *slot[k];
+            hsflow_ctx *ctx = slot[k]->ctx;
             for (int j = k; j < batch && r == HSFLOW_OK; j += nw)
                 r = hsflow_flow(ctx, I0[j], I1[j], dtype_in, rows, cols, in_step0, in_step1,
                                 window, iters, alpha, u[j], v[j], dtype_out, out_step);
-            if (r) msg[k] = hsflow_last_error(ctx);
+            if (r) {
+                msg[k] = hsflow_last_error(ctx);
+                // a context that hit an error is not trusted with the next call
+                hsflow_destroy(ctx);
+                slot[k]->ctx = nullptr;
+            }
             rc[k] = r;
         });
     }
@@ -873,6 +862,16 @@ int hsflow_flow_multi(const int *devices, int n_devices, int batch,
     for (int k = 0; k < nw; ++k)
         if (rc[k]) return fail(nullptr, rc[k], "device %d: %s", devices[k], msg[k].c_str());
     return HSFLOW_OK;
+}
+
+void hsflow_flow_multi_release(void) {
+    std::lock_guard<std::mutex> reg(g_multi_mu);
+    for (auto &dv : g_multi)
+        for (auto &sl : dv) {
+            std::lock_guard<std::mutex> hold(sl->mu);
+            if (sl->ctx) hsflow_destroy(sl->ctx);
+            sl->ctx = nullptr;
+        }
 }
 
 int hsflow_pyramid_level_size(int rows, int cols, int level, int *level_rows,
@@ -968,16 +967,18 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
     if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, wsb))) return rc;
     char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
     float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
-    int dt0 = 0, dt1 = 0;
-    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step0, in0, &dt0))) return rc;
-    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step1, in1, &dt1))) return rc;
+    const size_t up_bytes = 2 * n * in_es;
+    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 2, n)))) return rc;
+    if ((rc = upload_pair(ctx, I0, I1, (int)in_es, rows, cols, in_step0, in_step1, in0, in1)))
+        return rc;
+    const int dt0 = dtype_in;
     rc = pyramid_impl(ctx, in0, in1, dt0, rows, cols, 1, levels, window, iters,
                       (float)alpha, du, dv, ctx->d_ws, ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
     {
         const float *srcs[2] = {du, dv};
         void *dsts[2] = {u, v};
-        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step, up_bytes)))
             return rc;
     }
     return HSFLOW_OK;
@@ -1042,10 +1043,10 @@ int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, i
     if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, hsflow_workspace_bytes(rows, cols, 1))))
         return rc;
     uint8_t *db = (uint8_t *)ctx->d_in, *dg = db + gray_off;
-    HIP_TRY(ctx, hipMemcpy2DAsync(db, (size_t)cols * 3, bgr0, bgr_step0, (size_t)cols * 3,
-                                  rows, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpy2DAsync(db + 3 * n, (size_t)cols * 3, bgr1, bgr_step1,
-                                  (size_t)cols * 3, rows, hipMemcpyHostToDevice, ctx->stream));
+    const size_t up_bytes = 6 * n;
+    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 2, n)))) return rc;
+    if ((rc = upload_pair(ctx, bgr0, bgr1, 3, rows, cols, bgr_step0, bgr_step1, db, db + 3 * n)))
+        return rc;
     hipError_t e = hsflow::launch_bgr2gray(db, rows, cols, 2, dg, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "bgr2gray launch");
     float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
@@ -1058,7 +1059,7 @@ int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, i
     {
         const float *srcs[2] = {du, dv};
         void *dsts[2] = {u, v};
-        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step, up_bytes)))
             return rc;
     }
     return HSFLOW_OK;
@@ -1082,16 +1083,18 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
     float *dx = (float *)ctx->d_out;
     float *dy = (float *)((char *)dx + align_up(n * 4));
     float *dt = (float *)((char *)dy + align_up(n * 4));
-    int dt0 = 0, dt1 = 0;
-    if ((rc = upload(ctx, I0, dtype_in, rows, cols, in_step0, in0, &dt0))) return rc;
-    if ((rc = upload(ctx, I1, dtype_in, rows, cols, in_step1, in1, &dt1))) return rc;
+    const size_t up_bytes = 2 * n * in_es;
+    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 3, n)))) return rc;
+    if ((rc = upload_pair(ctx, I0, I1, (int)in_es, rows, cols, in_step0, in_step1, in0, in1)))
+        return rc;
+    const int dt0 = dtype_in;
     rc = gradients_impl(ctx, in0, in1, dt0, rows, cols, 1, dx, dy, dt, ctx->d_ws,
                         ctx->d_ws_bytes, ctx->stream);
     if (rc) return rc;
     {
         const float *srcs[3] = {dx, dy, dt};
         void *dsts[3] = {gx, gy, gt};
-        if ((rc = download_planes(ctx, srcs, dsts, 3, rows, cols, dtype_out, out_step)))
+        if ((rc = download_planes(ctx, srcs, dsts, 3, rows, cols, dtype_out, out_step, up_bytes)))
             return rc;
     }
     return HSFLOW_OK;

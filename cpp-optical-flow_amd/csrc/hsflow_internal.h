@@ -4,6 +4,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <vector>
+
 namespace hsflow {
 
 // Arguments of one Jacobi launch (hornSchunck.cpp:56-74 x `iters`).
@@ -49,7 +51,24 @@ int default_kb(int W);
 int fill_kb(int W, int kb, int rows, int cols, int batch);
 bool kb_supported(int W, int KB, bool need_f32);
 // the solve's launches leave most of the chip idle (all pairs in flight):
-// their outputs are stored write-through (JacobiArgs::write_through)
-bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch);
+// their outputs are stored write-through (JacobiArgs::write_through);
+// strip_rows = the K4 segment height the launches use (0: 84)
+bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch, int strip_rows);
+
+// ---- host I/O of the host-buffer entry points (hsflow_hostio.cpp) ----
+// threads of the host copy pool (the caller included)
+int host_pool_width();
+// n host frames (row steps step[k], elem bytes per pixel) -> dense device
+// planes dst[k], staged through `stage` (n * rows * cols * elem pinned bytes)
+// in row chunks; returns once every chunk's H2D copy is queued on s
+hipError_t upload_frames(const void *const *src, const size_t *step, int n, int rows, int cols,
+                         int elem, void *const *dst, char *stage, hipStream_t s);
+// n dense device f32 planes -> host rows (f64 when `f64`, else f32; row step
+// `step`) through `stage` (n * rows * cols floats, pinned): pitched DMA copies
+// per row chunk, each widened / copied by the pool as soon as it has
+// arrived.  Returns when every row is in place (the stream has drained).
+hipError_t download_planes_pipelined(const float *const *src, void *const *dst, int n, int rows,
+                                     int cols, bool f64, size_t step, float *stage,
+                                     std::vector<hipEvent_t> &events, hipStream_t s);
 
 }  // namespace hsflow

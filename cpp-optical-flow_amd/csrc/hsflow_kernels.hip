@@ -1061,15 +1061,17 @@ int fill_kb(int W, int kb, int rows, int cols, int batch) {
     return t8 <= slots ? 8 : kb;
 }
 
-bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch) {
+bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch, int strip_rows) {
     if (rows <= 0 || cols <= 0 || batch <= 0) return false;
     JacobiArgs a{};
     a.rows = rows;
     a.cols = cols;
     a.batch = batch;
-    if (strip) {  // K4: under 3/4 of the wave slots (a 4K pair: 962 of 2048)
+    if (strip) {  // K4: under 3/4 of the wave slots (a 4K pair: 962 of 2048),
+                  // counted with the segment height the launch uses
         int nseg = 0, nstrips = 0;
-        strip_seg_rows(W, KB, rows, cols, batch, 1, &nseg, &nstrips, 84);
+        strip_seg_rows(W, KB, rows, cols, batch, 1, &nseg, &nstrips,
+                       strip_rows > 0 ? strip_rows : 84);
         return (long)nseg * nstrips * batch * 4 < 8L * device_cus() * 3;
     }
     // K2: one round of 8-wave tiles (a single 1080p pair: 460 for 512 slots)

@@ -239,8 +239,14 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // the row's byte offset goes in soffset, 2^31 for rows above the image
     // (no VALU work and no branches per load; a per-lane offset stays
     // constant).  Offsets stay below 2^32: voffset < 2^31, soffset <= 2^31.
+    // Rows below the image take 2^31 as well: their own byte offset can pass
+    // 2^31 for planes near the 2^29-pixel cap, and voffset kOOB + such an
+    // soffset would wrap past 2^32 back into the plane (one wave-uniform
+    // compare per row).
     const int row_bytes = cols * 4;
-    auto row_off = [&](int r) { return r >= 0 ? r * row_bytes : (int)0x80000000; };
+    auto row_off = [&](int r) {
+        return (unsigned)r < (unsigned)rows ? r * row_bytes : (int)0x80000000;
+    };
     auto issue = [&](RowIn<G32> &d, int r) { load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(r)); };
 
     RowIn<G32> buf[D];

@@ -52,6 +52,7 @@ EXPORTS = (
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
     "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
     "hsflow_download_device", "hsflow_jacobi_kernel_name", "hsflow_set_strip_rows",
+    "hsflow_flow_multi_release",
 )
 BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
 
@@ -136,6 +137,8 @@ def lib():
                                     ctypes.POINTER(_vp), i, i, i, _sz, _sz, i, i,
                                     ctypes.c_double, ctypes.POINTER(_vp),
                                     ctypes.POINTER(_vp), i, _sz]
+    L.hsflow_flow_multi_release.argtypes = []
+    L.hsflow_flow_multi_release.restype = None
     _lib = L
     return L
 
@@ -178,6 +181,13 @@ def _as_image(a) -> np.ndarray:
     return a
 
 
+def _reusable(out, shape, dtype) -> bool:
+    """(u, v) can take a solve's output in place: the create() rule."""
+    return all(isinstance(x, np.ndarray) and x.shape == tuple(shape) and
+               x.dtype == np.dtype(dtype) and x.flags.c_contiguous and x.flags.writeable
+               for x in out) and out[0] is not out[1]
+
+
 class Context:
     """Device + stream + cached device buffers (hsflow_ctx)."""
 
@@ -205,14 +215,29 @@ class Context:
         except Exception:
             pass
 
-    def flow(self, I0, I1, window: int, iters: int, alpha: float, out_dtype=np.float64):
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def flow(self, I0, I1, window: int, iters: int, alpha: float, out_dtype=np.float64,
+             out=None):
+        """getFlow on host arrays.  `out` = (u, v): C-contiguous rows x cols
+        arrays of out_dtype written in place (cv::Mat::create() keeps an
+        existing CV_64FC1 buffer of the right size the same way); else new
+        arrays."""
         a, b = _as_image(I0), _as_image(I1)
         if a.shape != b.shape:
             raise HsflowError(HSFLOW_ERR_SIZE, "Image sizes are different")
         a, b = _common_dtype(a, b)
         rows, cols = a.shape
-        u = np.empty((rows, cols), out_dtype)
-        v = np.empty((rows, cols), out_dtype)
+        if out is not None and _reusable(out, (rows, cols), out_dtype):
+            u, v = out
+        else:
+            u = np.empty((rows, cols), out_dtype)
+            v = np.empty((rows, cols), out_dtype)
         code = F64 if u.dtype == np.float64 else F32
         rc = lib().hsflow_flow(self._p, a.ctypes.data, b.ctypes.data, _dtype_code(a),
                                rows, cols, a.strides[0], b.strides[0], int(window),
@@ -336,6 +361,11 @@ def flow_multi(devices, pairs, window: int, iters: int, alpha: float,
     return out
 
 
+def flow_multi_release():
+    """Destroy the per-device contexts flow_multi keeps (hsflow_flow_multi_release)."""
+    lib().hsflow_flow_multi_release()
+
+
 def default_context() -> Context:
     global _default_ctx
     if _default_ctx is None:
@@ -366,12 +396,15 @@ class hornSchunck:  # noqa: N801  (reference class name, hornSchunck.cpp:8)
         return gx, gy, gt
 
     def getFlow(self, imagePrev, imageNext, u=None, v=None):
-        """hornSchunck.cpp:43-75 -> (u, v) float64 (CV_64FC1)."""
+        """hornSchunck.cpp:43-75 -> (u, v) float64 (CV_64FC1).  Given u, v
+        float64 arrays of the frame size, the solve writes into them (as the
+        cv::Mat adapter's create() does); other arrays receive a copy."""
+        out = (u, v) if u is not None and v is not None else None
         uu, vv = self._c().flow(imagePrev, imageNext, self.windowSize,
-                                self.maxIterations, self.alpha)
-        if u is not None:
+                                self.maxIterations, self.alpha, out=out)
+        if u is not None and u is not uu:
             u[...] = uu
-        if v is not None:
+        if v is not None and v is not vv:
             v[...] = vv
         return uu, vv
 

@@ -104,12 +104,19 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,
  * may be listed twice (two streams on one GPU).  Blocking; returns the
  * first error, its message in hsflow_last_error(NULL).  The per-device
  * contexts are kept by the library across calls (no allocation or device
- * synchronisation per call once warm); concurrent calls are serialised. */
+ * synchronisation per call once warm); a context whose call failed is
+ * destroyed, not reused.  Concurrent calls that list the same device slot
+ * are serialised on that slot only. */
 int hsflow_flow_multi(const int *devices, int n_devices, int batch,
                       const void *const *I0, const void *const *I1, int dtype_in, int rows,
                       int cols, size_t in_step0, size_t in_step1, int window, int iters,
                       double alpha, void *const *u, void *const *v, int dtype_out,
                       size_t out_step);
+
+/* Destroys every context hsflow_flow_multi keeps (device buffers, pinned
+ * stages, streams); the next multi call creates them again.  Waits for
+ * multi calls in progress. */
+void hsflow_flow_multi_release(void);
 
 /* hornSchunck::getGradients (hornSchunck.cpp:19-41): gx, gy, gt. */
 int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in,

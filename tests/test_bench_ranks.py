@@ -93,3 +93,67 @@ def test_stream_leg_gathers_every_pair_in_order_one_rank():
     args = types.SimpleNamespace(iters=0, pairs=3, steps=1, window=5, alpha=1.0)
     leg = bench.stream_leg("tiny", args, 1, 0, torch.device("cpu"), solve_batch=_solve_batch)
     assert leg["gathered"] == 3 and leg["finite"] and leg["transport"] == "none (one rank)"
+
+
+# ------------------------------------------------------- config-5 bands leg
+B_ROWS, B_COLS, B_LEVELS, B_ITERS, B_CHUNK = 104, 45, 2, 8, 3
+
+
+def _bands_worker(rank, world, port, q, overlap):
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, ROOT, os.path.join(ROOT, "oracle"),
+                    os.path.join(ROOT, "cpp-optical-flow_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from test_row_bands import OracleOps
+        bench.WORKLOADS["tinyb"] = dict(rows=B_ROWS, cols=B_COLS, iters=B_ITERS, batch=1,
+                                        levels=B_LEVELS, dtype="f32")
+        args = types.SimpleNamespace(workload="tinyb", iters=0, levels=0, dtype=None,
+                                     window=5, alpha=1.0, chunk=B_CHUNK, overlap=overlap,
+                                     mode="resident")
+        out = []
+        leg = bench.bands_leg(args, world, rank, torch.device("cpu"), steps=2, warmup=1,
+                              ops=OracleOps(5, 1.0), result=out)
+        q.put((rank, leg, out[0] if out else None))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_bench_bands_leg_over_gloo(overlap):
+    """bench.bands_leg -- the default run's configs[4] leg at N > 1 -- with 2
+    ranks over gloo: frames broadcast from rank 0, row bands with the halo
+    exchange after every chunk (the code RCCL runs), timed with the driver's
+    rule, rank 0 gathers; the gathered (u, v) equal the undivided solve bit
+    for bit (the CPU oracle is the band solver here, libhsflow on the GPU)."""
+    sys.path[:0] = [ROOT]
+    import oracle
+    from synth_ref import synth_pair
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bands_worker, args=(r, world, port, q, overlap))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, leg, uv = q.get(timeout=240)
+        res[rank] = (leg, uv)
+    for p in procs:
+        p.join(timeout=60)
+    leg0, leg1 = res[0][0], res[1][0]
+    assert isinstance(leg0, dict) and isinstance(leg1, dict), (leg0, leg1)
+    assert leg0["n_ranks"] == 2 and leg0["transport"] == "gloo (cpu tensors)"
+    assert leg0["exchanges_per_solve"] == B_LEVELS * -(-B_ITERS // B_CHUNK)
+    assert leg0["ms_per_pair"] == leg1["ms_per_pair"] > 0  # max over ranks
+    assert leg0["parity"]["ok"] is None  # no committed golden at this size
+    I0, I1 = synth_pair(1000, B_ROWS, B_COLS)
+    uo, vo = oracle.flow_pyramid(I0, I1, B_LEVELS, 5, B_ITERS, 1.0)
+    u, v = res[0][1]
+    assert np.array_equal(u, uo) and np.array_equal(v, vo)

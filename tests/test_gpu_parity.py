@@ -462,3 +462,93 @@ def test_16k_square_plane_offsets(hs):
     assert norm_rel_err(a[0][r0 + 24:n - 1, c0 + 24:n - 1], uo[24:h - 1, 24:w - 1]) <= TOL
     del t0, t1
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------ round 4: wider full-size parity
+def test_full_size_alpha5_window4_against_oracle(hs):
+    """A full 1080p frame off the defaults: alpha 5 (hornSchunck.cpp:68,
+    alpha^2 in the denominator) and the even window 4 (anchor w - w/2 - 1 = 1,
+    hornSchunck.cpp:53-54: an asymmetric 4x4 box), 50 iterations, against
+    the float64 oracle."""
+    import torch
+    I0, I1 = hs.synth_pair(1000, 1080, 1920)
+    u, v = hs.flow_device(torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda(),
+                          4, 50, 5.0)
+    uo, vo = oracle.flow(I0, I1, 4, 50, 5.0, nthreads=16)
+    eu, ev = norm_rel_err(u.cpu().numpy(), uo), norm_rel_err(v.cpu().numpy(), vo)
+    print(f"1080p alpha 5 w 4 x 50: max|du|/max|u| = {eu:.2e}, dv {ev:.2e}")
+    assert eu <= TOL and ev <= TOL
+
+
+# ------------------------------- round 4: the pipelined host-buffer path
+@pytest.mark.parametrize("shape", [(1080, 1920), (1081, 1923), (37, 2050), (300, 49)])
+def test_host_api_pipelined_io_bits(hs, ctx, shape):
+    """hsflow_flow's chunked upload / download (hsflow_hostio.cpp) returns
+    the device solve's bits: f64 outputs are the f32 solve widened, f32
+    outputs equal it, reused output buffers (the cv::Mat::create path) equal
+    fresh ones, and a strided (ROI) input equals its dense copy."""
+    import torch
+    rows, cols = shape
+    I0, I1 = hs.synth_pair(77, rows, cols, dtype=np.uint8)
+    ud, vd = hs.flow_device(torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda(), 5, 24, 1.0)
+    ud, vd = ud.cpu().numpy(), vd.cpu().numpy()
+    u, v = ctx.flow(I0, I1, 5, 24, 1.0)
+    assert u.dtype == np.float64
+    assert np.array_equal(u, ud.astype(np.float64)) and np.array_equal(v, vd.astype(np.float64))
+    u32, v32 = ctx.flow(I0, I1, 5, 24, 1.0, out_dtype=np.float32)
+    assert np.array_equal(u32, ud) and np.array_equal(v32, vd)
+    ur = np.full((rows, cols), np.nan)
+    vr = np.full((rows, cols), np.nan)
+    got = hs.hornSchunck(5, 24, 1.0, context=ctx).getFlow(I0, I1, ur, vr)
+    assert got[0] is ur and got[1] is vr  # written in place
+    assert np.array_equal(ur, u) and np.array_equal(vr, v)
+    big0 = np.zeros((rows + 3, cols + 5), np.uint8)
+    big1 = np.zeros_like(big0)
+    big0[2:2 + rows, 3:3 + cols] = I0
+    big1[2:2 + rows, 3:3 + cols] = I1
+    ur2, vr2 = ctx.flow(big0[2:2 + rows, 3:3 + cols], big1[2:2 + rows, 3:3 + cols], 5, 24, 1.0)
+    assert np.array_equal(ur2, u) and np.array_equal(vr2, v)
+
+
+def test_host_api_concurrent_contexts(hs):
+    """Several host threads, each with its own context, call hsflow_flow at
+    once (the copy pool serves one of them, the others copy inline): every
+    result equals the same pair solved alone."""
+    import threading
+    pairs = [hs.synth_pair(500 + k, 540, 960, dtype=np.uint8) for k in range(4)]
+    ref = []
+    with hs.Context(0) as c0:
+        for I0, I1 in pairs:
+            ref.append(c0.flow(I0, I1, 5, 30, 1.0))
+    out = [None] * len(pairs)
+    errs = []
+
+    def run(k):
+        try:
+            with hs.Context(0) as c:
+                for _ in range(3):
+                    out[k] = c.flow(pairs[k][0], pairs[k][1], 5, 30, 1.0)
+        except Exception as e:  # pragma: no cover
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(len(pairs))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errs, errs
+    for k in range(len(pairs)):
+        assert np.array_equal(out[k][0], ref[k][0]) and np.array_equal(out[k][1], ref[k][1])
+
+
+def test_flow_multi_release_and_reuse(hs, ctx):
+    """hsflow_flow_multi_release drops the kept per-device contexts; the next
+    multi call builds them again and gives the same bits."""
+    pairs = [hs.synth_pair(900 + k, 200, 310, dtype=np.uint8) for k in range(3)]
+    a = hs.flow_multi([0, 0], pairs, 5, 20, 1.0)
+    hs.flow_multi_release()
+    b = hs.flow_multi([0], pairs, 5, 20, 1.0)
+    for (ua, va), (ub, vb), (I0, I1) in zip(a, b, pairs):
+        uc, vc = ctx.flow(I0, I1, 5, 20, 1.0)
+        assert np.array_equal(ua, ub) and np.array_equal(va, vb)
+        assert np.array_equal(ua, uc) and np.array_equal(va, vc)

@@ -130,3 +130,26 @@ def test_float64_device_tensors(hs):
     u32, v32 = hs.flow_device(t0.float(), t1.float(), 5, 30, 1.0)
     torch.cuda.synchronize()
     assert torch.equal(u64, u32) and torch.equal(v64, v32)  # integral frames: same bits
+
+
+@pytest.mark.parametrize("cols", [4096, 4097])
+def test_k4_bits_equal_k2_at_the_plane_size_cap(hs, cols):
+    """A plane within a few rows of the 2^29-pixel cap (2 GiB of f32 per
+    plane): K4 streams up to KB AR + D rows past the bottom edge, whose byte
+    offsets pass 2^31; those rows must still read as zero in every lane
+    (also the lanes outside the image columns), so K4 keeps K2's bits down
+    to the last row.  Random u8 frames made on the device; one 6-iteration
+    pass."""
+    rows = ((1 << 29) - 1) // cols
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    I0 = torch.randint(0, 256, (1, rows, cols), dtype=torch.uint8, device="cuda", generator=g)
+    I1 = torch.randint(0, 256, (1, rows, cols), dtype=torch.uint8, device="cuda", generator=g)
+    a = _solve(hs, 2, I0, I1, 5, 6)
+    b = _solve(hs, 4, I0, I1, 5, 6)
+    for x, y in zip(a, b):
+        assert torch.equal(x[0, -256:], y[0, -256:]), "bottom rows differ"
+        assert torch.equal(x, y)
+        assert bool(torch.isfinite(y[0, -256:]).all())
+    del a, b, I0, I1
+    torch.cuda.empty_cache()
