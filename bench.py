@@ -1073,7 +1073,9 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     levels = args.levels or wl.get("levels", 1)
     in_dtype = args.dtype or wl.get("dtype", "f32")
     window, alpha = args.window, args.alpha
-    chunk = chunk or args.chunk
+    # one rank exchanges nothing: its band is the whole plane, solved in one
+    # call per level
+    chunk = chunk or (args.chunk if world > 1 else iters)
     tdt = {"f16": torch.float16, "f32": torch.float32, "u8": torch.uint8}[in_dtype]
     I0 = torch.empty((rows, cols), dtype=tdt, device=dev)
     I1 = torch.empty_like(I0)

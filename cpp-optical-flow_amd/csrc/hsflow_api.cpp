@@ -35,7 +35,7 @@ struct hsflow_ctx {
     size_t d_out_bytes = 0;  // holds u, v (or gx, gy, gt)
     void *d_ws = nullptr;
     size_t d_ws_bytes = 0;
-    // pinned host staging: [uploaded frames][downloaded f32 planes]
+    // pinned host staging of f32 planes on their way to f64 rows
     char *h_stage = nullptr;
     size_t h_stage_bytes = 0;
     // one event per downloaded row chunk (created on first use)
@@ -455,36 +455,34 @@ int grow_host(hsflow_ctx *ctx, size_t need) {
     return HSFLOW_OK;
 }
 
-// Pinned stage layout of a host-buffer call: the uploaded frames first, the
-// downloaded planes after them (both used within one call, which ends with
-// the stream drained).
-size_t stage_bytes(size_t up_bytes, int n_down, size_t plane_px) {
-    return align_up(up_bytes) + (size_t)n_down * plane_px * 4;
-}
-
 // Two host frames (any supported dtype, any row steps) -> dense device rows
-// of the same type, through the pinned stage in row chunks
-// (hsflow_hostio.cpp; K1 takes the Sobel sums of CV_64FC1 frames in float64,
-// as hornSchunck.cpp:23-28 do, and rounds each gradient to f32 once).
+// of the same type (K1 takes the Sobel sums of CV_64FC1 frames in float64,
+// as hornSchunck.cpp:23-28 do, and rounds each gradient to f32 once).  The
+// runtime's own pageable upload is the fastest route measured
+// (hsflow_hostio.cpp).
 int upload_pair(hsflow_ctx *ctx, const void *I0, const void *I1, int elem, int rows, int cols,
                 size_t step0, size_t step1, void *dst0, void *dst1) {
-    const void *src[2] = {I0, I1};
-    const size_t step[2] = {step0, step1};
-    void *dst[2] = {dst0, dst1};
-    HIP_TRY(ctx, hsflow::upload_frames(src, step, 2, rows, cols, elem, dst, ctx->h_stage,
-                                       ctx->stream));
+    const size_t rb = (size_t)cols * elem;
+    HIP_TRY(ctx, hipMemcpy2DAsync(dst0, rb, I0, step0, rb, rows, hipMemcpyHostToDevice,
+                                  ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(dst1, rb, I1, step1, rb, rows, hipMemcpyHostToDevice,
+                                  ctx->stream));
     return HSFLOW_OK;
 }
 
-// n dense device f32 planes -> host rows of dtype_out with step `step`: row
-// chunks downloaded by DMA into the stage behind the uploaded frames and
-// widened (or copied) by the host pool as they arrive.
+// n dense device f32 planes -> host rows of dtype_out with step `step`
+// (hsflow_hostio.cpp: f32 straight down, f64 through the pinned stage,
+// widened by the host pool chunk by chunk as the copies land).
 int download_planes(hsflow_ctx *ctx, const float *const *src, void *const *dst, int n,
-                    int rows, int cols, int dtype_out, size_t step, size_t up_bytes) {
-    float *stage = (float *)(ctx->h_stage + align_up(up_bytes));
-    HIP_TRY(ctx, hsflow::download_planes_pipelined(src, dst, n, rows, cols,
-                                                   dtype_out == HSFLOW_F64, step, stage,
-                                                   ctx->dl_ev, ctx->stream));
+                    int rows, int cols, int dtype_out, size_t step) {
+    const bool f64 = dtype_out == HSFLOW_F64;
+    if (f64) {
+        int rc = grow_host(ctx, (size_t)n * rows * cols * 4);
+        if (rc) return rc;
+    }
+    HIP_TRY(ctx, hsflow::download_planes_pipelined(src, dst, n, rows, cols, f64, step,
+                                                   (float *)ctx->h_stage, ctx->dl_ev,
+                                                   ctx->stream));
     return HSFLOW_OK;
 }
 
@@ -785,8 +783,6 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, wsb))) return rc;
     char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
     float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
-    const size_t up_bytes = 2 * n * in_es;
-    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 2, n)))) return rc;
     if ((rc = upload_pair(ctx, I0, I1, (int)in_es, rows, cols, in_step0, in_step1, in0, in1)))
         return rc;
     const int dt0 = dtype_in;
@@ -799,7 +795,7 @@ int hsflow_flow(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in, i
     {
         const float *srcs[2] = {du, dv};
         void *dsts[2] = {u, v};
-        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step, up_bytes)))
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
             return rc;
     }
     return HSFLOW_OK;
@@ -967,8 +963,6 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
     if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, wsb))) return rc;
     char *in0 = (char *)ctx->d_in, *in1 = in0 + align_up(n * in_es);
     float *du = (float *)ctx->d_out, *dv = (float *)((char *)du + align_up(n * 4));
-    const size_t up_bytes = 2 * n * in_es;
-    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 2, n)))) return rc;
     if ((rc = upload_pair(ctx, I0, I1, (int)in_es, rows, cols, in_step0, in_step1, in0, in1)))
         return rc;
     const int dt0 = dtype_in;
@@ -978,7 +972,7 @@ int hsflow_flow_pyramid(hsflow_ctx *ctx, const void *I0, const void *I1, int dty
     {
         const float *srcs[2] = {du, dv};
         void *dsts[2] = {u, v};
-        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step, up_bytes)))
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
             return rc;
     }
     return HSFLOW_OK;
@@ -1043,8 +1037,6 @@ int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, i
     if ((rc = grow(ctx, &ctx->d_ws, &ctx->d_ws_bytes, hsflow_workspace_bytes(rows, cols, 1))))
         return rc;
     uint8_t *db = (uint8_t *)ctx->d_in, *dg = db + gray_off;
-    const size_t up_bytes = 6 * n;
-    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 2, n)))) return rc;
     if ((rc = upload_pair(ctx, bgr0, bgr1, 3, rows, cols, bgr_step0, bgr_step1, db, db + 3 * n)))
         return rc;
     hipError_t e = hsflow::launch_bgr2gray(db, rows, cols, 2, dg, ctx->stream);
@@ -1059,7 +1051,7 @@ int hsflow_flow_bgr(hsflow_ctx *ctx, const uint8_t *bgr0, const uint8_t *bgr1, i
     {
         const float *srcs[2] = {du, dv};
         void *dsts[2] = {u, v};
-        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step, up_bytes)))
+        if ((rc = download_planes(ctx, srcs, dsts, 2, rows, cols, dtype_out, out_step)))
             return rc;
     }
     return HSFLOW_OK;
@@ -1083,8 +1075,6 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
     float *dx = (float *)ctx->d_out;
     float *dy = (float *)((char *)dx + align_up(n * 4));
     float *dt = (float *)((char *)dy + align_up(n * 4));
-    const size_t up_bytes = 2 * n * in_es;
-    if ((rc = grow_host(ctx, stage_bytes(up_bytes, 3, n)))) return rc;
     if ((rc = upload_pair(ctx, I0, I1, (int)in_es, rows, cols, in_step0, in_step1, in0, in1)))
         return rc;
     const int dt0 = dtype_in;
@@ -1094,7 +1084,7 @@ int hsflow_gradients(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_
     {
         const float *srcs[3] = {dx, dy, dt};
         void *dsts[3] = {gx, gy, gt};
-        if ((rc = download_planes(ctx, srcs, dsts, 3, rows, cols, dtype_out, out_step, up_bytes)))
+        if ((rc = download_planes(ctx, srcs, dsts, 3, rows, cols, dtype_out, out_step)))
             return rc;
     }
     return HSFLOW_OK;

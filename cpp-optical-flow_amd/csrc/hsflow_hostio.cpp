@@ -3,20 +3,16 @@
 // cv::Mat drop-in takes for main.cpp:97-98 (frames in pageable host memory,
 // u and v back as CV_64FC1, hornSchunck.cpp:49-50, 72-73).
 //
-// Both directions go through the context's pinned stage in row chunks, so
-// the DMA engines and the host threads work at the same time:
-//   upload    pool threads copy the caller's rows into the stage chunk by
-//             chunk; each chunk's H2D copy is queued as soon as its rows
-//             are staged (the runtime's own pageable path stages through a
-//             single thread);
-//   download  every chunk of every plane is queued at once as a pitched DMA
-//             copy (the runtime gives pitched device -> pinned copies its
-//             DMA engines: ~46 GB/s against ~29 GB/s flat,
-//             scripts/pcie/d2h_engine_probe.hip) with an event behind it;
-//             pool threads widen f32 -> f64 (or copy f32) chunk k into the
-//             caller's rows as soon as its event has fired, while later
-//             chunks are still in flight.
-// Only the last chunk's widening is left after the last DMA copy.
+// Measured phase costs of a 1080p pair (profiles/r04_hostio_probe.txt,
+// scripts/pcie/hostio_probe.cpp): the runtime's own pageable H2D of the two
+// u8 frames 0.09 ms (staging them through a pinned buffer first: 0.16 ms);
+// the D2H of the two f32 planes 0.31 ms, pageable or pinned alike; widening
+// them to f64 on the host 1.73 ms on one thread, 0.44 ms on eight.  So the
+// frames go up as they are, f32 results come down straight into the
+// caller's rows, and only f64 (CV_64FC1, the reference's output type) goes
+// through the pinned stage: the planes come down in row chunks with an event
+// behind each, and the whole pool widens chunk k while chunks k+1.. are
+// still in flight; only the last chunk's widening follows the last copy.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -120,47 +116,32 @@ private:
     unsigned long gen_ = 0;
 };
 
-// rows per chunk: ~256 K pixels (1 MB of f32), at most 32 chunks per plane
-int chunk_rows(int rows, int cols) {
-    const long px = 256L * 1024;
-    int r = (int)std::max<long>(1, px / std::max(1, cols));
-    r = std::max(r, (rows + 31) / 32);
-    return std::min(r, rows);
-}
-
 }  // namespace
 
 int host_pool_width() { return Pool::get().width(); }
 
-hipError_t upload_frames(const void *const *src, const size_t *step, int n, int rows, int cols,
-                         int elem, void *const *dst, char *stage, hipStream_t s) {
-    const size_t row_bytes = (size_t)cols * elem;
-    const int cr = chunk_rows(rows, cols);
-    const int per = (rows + cr - 1) / cr;
-    std::atomic<int> err{(int)hipSuccess};
-    Pool::get().run(n * per, [&](int i) {
-        const int k = i / per, c = i % per;
-        const int r0 = c * cr, r1 = std::min(rows, r0 + cr);
-        char *st = stage + (size_t)k * rows * row_bytes + (size_t)r0 * row_bytes;
-        const char *sp = (const char *)src[k] + (size_t)r0 * step[k];
-        if (step[k] == row_bytes) {
-            std::memcpy(st, sp, (size_t)(r1 - r0) * row_bytes);
-        } else {
-            for (int r = r0; r < r1; ++r)
-                std::memcpy(st + (size_t)(r - r0) * row_bytes, sp + (size_t)(r - r0) * step[k],
-                            row_bytes);
-        }
-        hipError_t e = hipMemcpyAsync((char *)dst[k] + (size_t)r0 * row_bytes, st,
-                                      (size_t)(r1 - r0) * row_bytes, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) err.store((int)e);
-    });
-    return (hipError_t)err.load();
-}
-
 hipError_t download_planes_pipelined(const float *const *src, void *const *dst, int n, int rows,
                                      int cols, bool f64, size_t step, float *stage,
                                      std::vector<hipEvent_t> &events, hipStream_t s) {
-    const int cr = chunk_rows(rows, cols);
+    const size_t row_bytes = (size_t)cols * 4;
+    if (!f64) {
+        // f32 rows need no host work: one pitched DMA copy per plane straight
+        // into the caller's rows (pageable memory downloads as fast as pinned
+        // here: 0.314 vs 0.311 ms for a 1080p pair, profiles/r04_hostio_probe.txt)
+        for (int k = 0; k < n; ++k) {
+            hipError_t e = hipMemcpy2DAsync(dst[k], step, src[k], row_bytes, row_bytes,
+                                            (size_t)rows, hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipStreamSynchronize(s);
+    }
+    // f64: each plane in kChunks row chunks (more chunks cost more DMA setup
+    // than they hide: 2 / 4 / 8 / 16 chunks per plane 0.354 / 0.407 / 0.522 /
+    // 0.767 ms against 0.311 ms in one copy, same probe), every chunk widened
+    // by ALL pool threads as soon as it has landed (one thread widens a 1080p
+    // pair at ~19 GB/s of writes, eight at ~110 GB/s)
+    constexpr int kChunks = 4, kSlices = 8;
+    const int cr = (rows + kChunks - 1) / kChunks;
     const int per = (rows + cr - 1) / cr;
     const int total = n * per;
     while ((int)events.size() < total) {
@@ -170,9 +151,6 @@ hipError_t download_planes_pipelined(const float *const *src, void *const *dst, 
         events.push_back(ev);
     }
     const size_t plane = (size_t)rows * cols;
-    const size_t row_bytes = (size_t)cols * 4;
-    // every chunk's DMA copy first, in plane-major order (the order the
-    // widening consumes them)
     for (int i = 0; i < total; ++i) {
         const int k = i / per, c = i % per;
         const int r0 = c * cr, r1 = std::min(rows, r0 + cr);
@@ -182,8 +160,11 @@ hipError_t download_planes_pipelined(const float *const *src, void *const *dst, 
         if (e == hipSuccess) e = hipEventRecord(events[i], s);
         if (e != hipSuccess) return e;
     }
+    // work items in chunk order, kSlices row slices per chunk: the pool's
+    // threads all wait for chunk 0, widen it together, then chunk 1, ...
     std::atomic<int> err{(int)hipSuccess};
-    Pool::get().run(total, [&](int i) {
+    Pool::get().run(total * kSlices, [&](int item) {
+        const int i = item / kSlices, sl = item % kSlices;
         hipError_t e = hipEventSynchronize(events[i]);
         if (e != hipSuccess) {
             err.store((int)e);
@@ -191,21 +172,15 @@ hipError_t download_planes_pipelined(const float *const *src, void *const *dst, 
         }
         const int k = i / per, c = i % per;
         const int r0 = c * cr, r1 = std::min(rows, r0 + cr);
+        const int h = r1 - r0, q0 = r0 + h * sl / kSlices, q1 = r0 + h * (sl + 1) / kSlices;
         const float *sp = stage + k * plane;
-        for (int r = r0; r < r1; ++r) {
+        for (int r = q0; r < q1; ++r) {
             const float *row = sp + (size_t)r * cols;
-            char *d = (char *)dst[k] + (size_t)r * step;
-            if (f64) {
-                double *dd = (double *)d;
-                for (int x = 0; x < cols; ++x) dd[x] = (double)row[x];
-            } else {
-                std::memcpy(d, row, row_bytes);
-            }
+            double *d = (double *)((char *)dst[k] + (size_t)r * step);
+            for (int x = 0; x < cols; ++x) d[x] = (double)row[x];
         }
     });
-    if (err.load() != (int)hipSuccess) return (hipError_t)err.load();
-    // the stream is idle now (the last event fired): later work may reuse the stage
-    return hipSuccess;
+    return (hipError_t)err.load();
 }
 
 }  // namespace hsflow

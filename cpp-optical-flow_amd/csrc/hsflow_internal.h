@@ -58,15 +58,11 @@ bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch, int 
 // ---- host I/O of the host-buffer entry points (hsflow_hostio.cpp) ----
 // threads of the host copy pool (the caller included)
 int host_pool_width();
-// n host frames (row steps step[k], elem bytes per pixel) -> dense device
-// planes dst[k], staged through `stage` (n * rows * cols * elem pinned bytes)
-// in row chunks; returns once every chunk's H2D copy is queued on s
-hipError_t upload_frames(const void *const *src, const size_t *step, int n, int rows, int cols,
-                         int elem, void *const *dst, char *stage, hipStream_t s);
 // n dense device f32 planes -> host rows (f64 when `f64`, else f32; row step
-// `step`) through `stage` (n * rows * cols floats, pinned): pitched DMA copies
-// per row chunk, each widened / copied by the pool as soon as it has
-// arrived.  Returns when every row is in place (the stream has drained).
+// `step`).  f32: DMA copies straight into the rows.  f64: through `stage`
+// (n * rows * cols floats, pinned) in row chunks, each widened by the pool
+// as soon as it has arrived.  Returns when every row is in place (the
+// stream has drained).
 hipError_t download_planes_pipelined(const float *const *src, void *const *dst, int n, int rows,
                                      int cols, bool f64, size_t step, float *stage,
                                      std::vector<hipEvent_t> &events, hipStream_t s);

@@ -160,7 +160,10 @@ class DeviceOps:
         with self._on():
             return self.torch.stack(planes)
 
-    def copy_many(self, dsts, srcs):
+    def copy_many(self, dsts, srcs, current=False):
+        if current:
+            self.torch._foreach_copy_(dsts, srcs)
+            return
         with self._on():
             self.torch._foreach_copy_(dsts, srcs)
 
@@ -218,7 +221,9 @@ class LocalComm:
                                              (su.V, su.SV, sd.V, sd.SV)):
                 d += [S_dn[sd.top][0:H], S_up[su.bot][2 * H:3 * H]]
                 x += [SB_up[su.bot], SB_dn[sd.top]]
-        self._met(states, lambda: _copy_many(states[0].ops, d, x))
+        # on the meeting stream itself (_met's caller's stream, which has
+        # waited for every rank): the copies read every rank's send buffers
+        self._met(states, lambda: _copy_many(states[0].ops, d, x, current=True))
         return None
 
     @staticmethod
@@ -352,11 +357,12 @@ def solve(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
     return states
 
 
-def _copy_many(ops, dsts, srcs):
+def _copy_many(ops, dsts, srcs, current=False):
     """dst[k][...] = src[k] for every k, in stream order (DeviceOps: one
-    fused launch)"""
+    fused launch, on the ops' stream -- or, with current, on the caller's
+    current stream)"""
     if hasattr(ops, "copy_many"):
-        ops.copy_many(dsts, srcs)
+        ops.copy_many(dsts, srcs, current=current)
     else:
         for d, x in zip(dsts, srcs):
             d[...] = x
@@ -588,14 +594,27 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
     streams must exist before a capture).  Returns (graph, u, v): each
     graph.replay() recomputes the level-0 (u, v) into u, v (rank 0's gather of
     the owned rows).  DistComm's RCCL point-to-point calls are not captured:
-    N real ranks run the schedules eagerly."""
+    N real ranks run the schedules eagerly.
+
+    Virtual ranks may run on streams of their own (DeviceOps(stream=...)):
+    each rank stream is forked from the capturing stream before the solve
+    issues anything on it, so its work joins the capture, and the solve's
+    last exchange / gather joins it back.  (Round 3 captured without that
+    fork: a rank stream's first operations ran uncaptured, and the
+    capturing stream then waited on an event recorded on that uncaptured
+    stream -- CUDA rejects such a wait with cudaErrorStreamCaptureIsolation;
+    this ROCm stack accepted it and crashed later inside
+    hipStreamEndCapture.  scripts/lab/capture_isolation.py reproduces both
+    orders.)"""
     import torch
     if not isinstance(comm, LocalComm):
         raise ValueError("graphed(): LocalComm virtual ranks only")
-    if any(o.stream is not None for o in ops_list):
-        # measured: capturing the overlapped schedule with a stream per
-        # virtual rank crashes inside hipStreamEndCapture on this stack
-        raise ValueError("graphed(): virtual ranks on the caller's stream only")
+    if solver is solve_overlapped and any(getattr(o, "stream", None) is not None
+                                          for o in ops_list):
+        # measured: still crashes inside hipStreamEndCapture on this stack
+        # (scripts/lab/capture_bisect.py, DESIGN.md §6)
+        raise ValueError("graphed(): the overlapped schedule takes virtual ranks on the "
+                         "caller's stream only")
     dev = ops_list[0].device
     side = torch.cuda.Stream(device=dev)
     side.wait_stream(torch.cuda.current_stream(dev))
@@ -605,6 +624,10 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
     torch.cuda.synchronize(dev)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        cap = torch.cuda.current_stream(dev)
+        for o in ops_list:  # fork every rank stream from the capture
+            if getattr(o, "stream", None) is not None:
+                o.stream.wait_stream(cap)
         st = solver(I0s, I1s, p, iters, ops_list, comm, ranks)
         u, v = gather_owned(st, p, comm)
     return g, u, v

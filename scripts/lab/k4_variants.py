@@ -1,0 +1,127 @@
+"""K4 lab variants: the product hsflow_strips.hip with textual patches, each
+linked with the product's other objects into cpp-optical-flow_amd/lab/
+libhsflow_<name>.so (not tracked; travels to the GPU box with the tree).
+
+    python scripts/lab/k4_variants.py build NAME [NAME ...]   # here (hipcc)
+    python scripts/lab/k4_variants.py probe NAME [NAME ...]   # GPU box
+
+Variants (timing questions about K4's issue limit):
+  base      the product source unchanged (the A/B reference build)
+  nop16     +16 `s_nop 0` per time step: does an instruction that is not
+            VALU cost the wave issue time (the K4 loop carries ~16 nops and
+            ~25 SALU per step)?
+  rawoff    loads and stores with the unclamped row offset r * row_bytes (no
+            compare / select per row): the most SALU trimming can give
+            (timing only; edge rows read garbage)
+`probe` runs 1080p x 8 and 4K x 2 solves (hipGraph replays after a 0.15 s
+pre-warm) with each build in its own process, alternating the order twice,
+and prints Mpix*iter/s per build."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+PKG = os.path.join(ROOT, "cpp-optical-flow_amd")
+LAB = os.path.join(PKG, "lab")
+SRC = os.path.join(PKG, "csrc", "hsflow_strips.hip")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fno-slp-vectorize"]
+
+PATCHES = {
+    "base": [],
+    "nop16": [("            __builtin_amdgcn_sched_barrier(0);\n",
+               "            asm volatile(\"s_nop 0\\n s_nop 0\\n s_nop 0\\n s_nop 0\\n"
+               " s_nop 0\\n s_nop 0\\n s_nop 0\\n s_nop 0\\n s_nop 0\\n s_nop 0\\n"
+               " s_nop 0\\n s_nop 0\\n s_nop 0\\n s_nop 0\\n s_nop 0\\n s_nop 0\");\n"
+               "            __builtin_amdgcn_sched_barrier(0);\n")],
+    "rawoff": [("        return (unsigned)r < (unsigned)rows ? r * row_bytes : (int)0x80000000;",
+                "        return r * row_bytes;"),
+               ("                    const int so = sin ? y * row_bytes : (int)0x80000000;",
+                "                    const int so = y * row_bytes; (void)sin;")],
+}
+
+
+def build(name):
+    os.makedirs(LAB, exist_ok=True)
+    src = open(SRC).read()
+    for old, new in PATCHES[name]:
+        assert old in src, (name, old)
+        src = src.replace(old, new)
+    path = os.path.join(PKG, "csrc", f"_lab_strips_{name}.hip")
+    with open(path, "w") as f:
+        f.write(src)
+    obj = os.path.join(LAB, f"strips_{name}.o")
+    try:
+        subprocess.check_call(["/opt/rocm/bin/hipcc", *FLAGS, "-c", path, "-o", obj])
+    finally:
+        os.remove(path)
+    objs = [os.path.join(PKG, "build", f) for f in sorted(os.listdir(os.path.join(PKG, "build")))
+            if f.endswith(".o") and f != "hsflow_strips.o"]
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o",
+                           os.path.join(LAB, f"libhsflow_{name}.so"), *objs, obj,
+                           "-Wl,-rpath,/opt/rocm/lib"])
+    print("built", name, flush=True)
+
+
+CHILD = r'''
+import os, sys, time, json
+sys.path.insert(0, %(pkg)r)
+import hsflow
+hsflow.LIB_PATH = %(lib)r
+import numpy as np, torch
+out = {}
+for tag, batch, rows, cols, iters in (("1080p8", 8, 1080, 1920, 300), ("4k2", 2, 2160, 3840, 500)):
+    ps = [hsflow.synth_pair(1000 + i, rows, cols) for i in range(batch)]
+    I0 = torch.from_numpy(np.stack([p[0] for p in ps])).cuda()
+    I1 = torch.from_numpy(np.stack([p[1] for p in ps])).cuda()
+    u = torch.empty((batch, rows, cols), dtype=torch.float32, device="cuda"); v = torch.empty_like(u)
+    ws = hsflow.alloc_workspace(rows, cols, batch)
+    s = torch.cuda.Stream(); s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws, s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws, torch.cuda.current_stream())
+    t = time.perf_counter(); n = 0
+    while time.perf_counter() - t < 0.15:
+        g.replay(); n += 1
+        if n %% 4 == 0: torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20): g.replay()
+    e1.record(); torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    out[tag] = {"ms": round(ms, 4), "Mpix_iter_s": round(batch * rows * cols * iters / ms / 1e3),
+                "u_sum": float(u.double().sum())}
+print("RESULT " + json.dumps(out), flush=True)
+'''
+
+
+def probe(names):
+    res = {n: [] for n in names}
+    order = list(names) + list(reversed(names))
+    for n in order:
+        lib = os.path.join(LAB, f"libhsflow_{n}.so")
+        code = CHILD % {"pkg": PKG, "lib": lib}
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                           timeout=240)
+        line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
+        if r.returncode != 0 or not line:
+            print(n, "FAILED", r.returncode, r.stderr[-2000:], flush=True)
+            return 1
+        res[n].append(json.loads(line[0][7:]))
+        print(n, line[0][7:], flush=True)
+    print(json.dumps({n: {k: max(x[k]["Mpix_iter_s"] for x in v) for k in v[0]}
+                      for n, v in res.items()}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    cmd, names = sys.argv[1], sys.argv[2:]
+    if cmd == "build":
+        for n in names:
+            build(n)
+    else:
+        sys.exit(probe(names))

@@ -1,0 +1,170 @@
+// Phase costs of the host-buffer path (hsflow_flow) for one 1080p pair:
+// upload of two u8 frames, download of two f32 planes, f32 -> f64 widening,
+// each in the variants the library could use.  Median of 15 per variant.
+//   hipcc -O2 -o hostio_probe scripts/pcie/hostio_probe.cpp -lpthread
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <thread>
+#include <vector>
+
+#define CK(x)                                                               \
+    do {                                                                    \
+        hipError_t e_ = (x);                                                \
+        if (e_ != hipSuccess) {                                             \
+            std::printf("%s: %s\n", #x, hipGetErrorString(e_));             \
+            std::exit(1);                                                   \
+        }                                                                   \
+    } while (0)
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+static double med(const std::function<void()> &f, int n = 15) {
+    f();
+    std::vector<double> t;
+    for (int i = 0; i < n; ++i) {
+        double a = now_ms();
+        f();
+        t.push_back(now_ms() - a);
+    }
+    std::sort(t.begin(), t.end());
+    return t[n / 2];
+}
+
+static void par(int nt, int n, const std::function<void(int)> &fn) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int i = t; i < n; i += nt) fn(i);
+        });
+    for (auto &x : th) x.join();
+}
+
+int main(int argc, char **argv) {
+    const int rows = argc > 1 ? atoi(argv[1]) : 1080, cols = argc > 2 ? atoi(argv[2]) : 1920;
+    const size_t n = (size_t)rows * cols;
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<uint8_t> f0(n, 1), f1(n, 2);  // pageable frames
+    std::vector<double> u(n), v(n);            // pageable outputs (warm)
+    std::memset(u.data(), 0, n * 8);
+    std::memset(v.data(), 0, n * 8);
+    uint8_t *dI;
+    float *dU;
+    CK(hipMalloc(&dI, 2 * n));
+    CK(hipMalloc(&dU, 2 * n * 4));
+    CK(hipMemset(dU, 0, 2 * n * 4));
+    char *pin;
+    CK(hipHostMalloc((void **)&pin, 2 * n + 2 * n * 4 + 4096, hipHostMallocDefault));
+    float *pst = (float *)(pin + ((2 * n + 4095) / 4096) * 4096);
+    std::vector<float> pagef(2 * n);
+    std::vector<hipEvent_t> ev(64);
+    for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipEvent_t evb;
+    CK(hipEventCreateWithFlags(&evb, hipEventDisableTiming | hipEventBlockingSync));
+
+    std::printf("%dx%d\n", cols, rows);
+    // ---- uploads
+    std::printf("up pageable 2x hipMemcpyAsync        %.3f ms\n", med([&] {
+        CK(hipMemcpyAsync(dI, f0.data(), n, hipMemcpyHostToDevice, s));
+        CK(hipMemcpyAsync(dI + n, f1.data(), n, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    std::printf("up memcpy->pinned (1 thr) + 1 H2D      %.3f ms\n", med([&] {
+        std::memcpy(pin, f0.data(), n);
+        std::memcpy(pin + n, f1.data(), n);
+        CK(hipMemcpyAsync(dI, pin, 2 * n, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    std::printf("up memcpy->pinned (8 thr) + 1 H2D      %.3f ms\n", med([&] {
+        par(8, 16, [&](int i) {
+            size_t c = 2 * n / 16;
+            std::memcpy(pin + i * c, (i < 8 ? f0.data() : f1.data()) + (i % 8) * c, c);
+        });
+        CK(hipMemcpyAsync(dI, pin, 2 * n, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    std::printf("up pinned H2D only (1 call)            %.3f ms\n", med([&] {
+        CK(hipMemcpyAsync(dI, pin, 2 * n, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    std::printf("up pinned H2D 16 chunks                %.3f ms\n", med([&] {
+        size_t c = 2 * n / 16;
+        for (int i = 0; i < 16; ++i)
+            CK(hipMemcpyAsync(dI + i * c, pin + i * c, c, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    // ---- downloads (2 planes, f32)
+    const size_t rb = (size_t)cols * 4;
+    std::printf("down flat 2x hipMemcpyAsync -> pinned  %.3f ms\n", med([&] {
+        CK(hipMemcpyAsync(pst, dU, n * 4, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(pst + n, dU + n, n * 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    std::printf("down pitched 2x 2D -> pinned           %.3f ms\n", med([&] {
+        CK(hipMemcpy2DAsync(pst, rb, dU, rb, rb, rows, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpy2DAsync(pst + n, rb, dU + n, rb, rb, rows, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    std::printf("down pitched 1x 2D both planes         %.3f ms\n", med([&] {
+        CK(hipMemcpy2DAsync(pst, rb, dU, rb, rb, 2 * rows, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    for (int per : {2, 4, 8, 16}) {
+        int cr = (rows + per - 1) / per;
+        std::printf("down pitched %2d chunks/plane + events  %.3f ms\n", per, med([&] {
+            int k = 0;
+            for (int p = 0; p < 2; ++p)
+                for (int r0 = 0; r0 < rows; r0 += cr, ++k) {
+                    int h = std::min(cr, rows - r0);
+                    CK(hipMemcpy2DAsync(pst + p * n + (size_t)r0 * cols, rb,
+                                        dU + p * n + (size_t)r0 * cols, rb, rb, h,
+                                        hipMemcpyDeviceToHost, s));
+                    CK(hipEventRecord(ev[k], s));
+                }
+            CK(hipEventSynchronize(ev[k - 1]));
+        }));
+    }
+    std::printf("down flat 2x -> pageable f32           %.3f ms\n", med([&] {
+        CK(hipMemcpyAsync(pagef.data(), dU, n * 4, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(pagef.data() + n, dU + n, n * 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+    }));
+    // ---- sync latency
+    std::printf("event sync (empty stream, default)     %.3f ms\n", med([&] {
+        CK(hipEventRecord(ev[0], s));
+        CK(hipEventSynchronize(ev[0]));
+    }));
+    std::printf("event sync (empty stream, blocking)    %.3f ms\n", med([&] {
+        CK(hipEventRecord(evb, s));
+        CK(hipEventSynchronize(evb));
+    }));
+    std::printf("stream sync (empty)                    %.3f ms\n",
+                med([&] { CK(hipStreamSynchronize(s)); }));
+    // ---- widening (warm output pages)
+    for (int nt : {1, 2, 4, 8, 16}) {
+        std::printf("widen f32->f64 2 planes, %2d threads    %.3f ms\n", nt, med([&] {
+            par(nt, 64, [&](int i) {
+                size_t c = 2 * n / 64, a = i * c;
+                for (size_t x = a; x < a + c; ++x) {
+                    if (x < n)
+                        u[x] = pst[x];
+                    else
+                        v[x - n] = pst[x];
+                }
+            });
+        }));
+    }
+    std::printf("thread spawn+join x7                   %.3f ms\n",
+                med([&] { par(7, 7, [](int) {}); }));
+    return 0;
+}

@@ -1,0 +1,149 @@
+"""Predicted N = 1/2/4/8 values of the two multi-GPU legs of bench.py, built
+from pieces measured on ONE GPU plus two stated link constants (the 8-GPU
+runs are the driver's; DESIGN.md §6 "Predictions" quotes this output).
+
+    python scripts/scale_predict.py > profiles/r04_scale_prediction.json
+
+stream leg (configs[3]): 64 1080p pairs held by rank 0; rank r solves pairs
+  r, r + N, ... in 2 groups (one at N = 1); rank 0 sends 2 x 8.3 MB of f32
+  frames per pair to its owner and receives 2 x 8.3 MB of (u, v) back.
+  Measured: the resident solve time of a 64/N-pair batch and of half of it.
+  Modelled: rank 0 sends the remote pairs over N - 1 links in parallel at
+  LINK_GBPS each (RCCL point-to-point over xGMI), the gather likewise; the
+  scatter precedes the first solve, group 0's gather overlaps group 1's
+  solve, group 1's gather is exposed.
+bands leg (configs[4] as stated for N GPUs): one 8K fp16 pair, 3 levels x
+  1000 it, rank r solves its extended band in chunks of `chunk` iterations
+  with a halo exchange after each.  Measured: per level, the GPU time and
+  the host issue time of one chunk on the largest extended band (eager
+  jacobi_device calls, as row_bands.solve issues them), K1 per level, the
+  pyramid build.  Modelled: an exchange costs XCHG_US of latency on the
+  critical path (2 x 2 RCCL sends and receives of H rows each, tiny) and the
+  host issues an exchange in XCHG_HOST_US; per chunk the slower of the GPU
+  (chunk + exchange) and the host (issue) sets the pace; the final gather
+  moves the owned rows of (u, v) to rank 0 at LINK_GBPS."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "cpp-optical-flow_amd"), ROOT]
+import hsflow  # noqa: E402
+import row_bands as rb  # noqa: E402
+
+LINK_GBPS = 50.0     # RCCL p2p per peer over one xGMI link (~1/3 of the 153 GB/s raw)
+XCHG_US = 40.0       # one halo exchange on the critical path (RCCL p2p latency)
+XCHG_HOST_US = 120.0  # host time to post one exchange (clones + batch_isend_irecv)
+
+
+def resident_ms(batch, reps=6):
+    rows, cols, iters = 1080, 1920, 300
+    ps = [hsflow.synth_pair(1000 + i, rows, cols) for i in range(batch)]
+    I0 = torch.from_numpy(np.stack([p[0] for p in ps])).cuda()
+    I1 = torch.from_numpy(np.stack([p[1] for p in ps])).cuda()
+    u = torch.empty((batch, rows, cols), dtype=torch.float32, device="cuda")
+    v = torch.empty_like(u)
+    ws = hsflow.alloc_workspace(rows, cols, batch)
+    hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws)
+    t_end = time.perf_counter() + 0.15
+    while time.perf_counter() < t_end:
+        hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws)
+        torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def stream_prediction(n, pairs=64):
+    per = pairs // n
+    groups = 2 if n > 1 else 1
+    t_all = resident_ms(per)
+    t_grp = resident_ms(max(1, per // groups)) if groups > 1 else t_all
+    mb = 2 * 1080 * 1920 * 4 / 1e6  # one direction, one pair
+    remote = pairs - per             # pairs rank 0 does not own
+    # rank 0 feeds n - 1 links at once; per link: per pairs
+    scatter = per * mb / LINK_GBPS if n > 1 else 0.0
+    gather_grp = (per // groups) * mb / LINK_GBPS if n > 1 else 0.0
+    if n == 1:
+        total = t_all
+    else:
+        total = scatter + t_grp + max(t_grp, gather_grp) + gather_grp
+    return {"n": n, "pairs_per_rank": per, "groups": groups,
+            "solve_ms_rank_share": round(t_all, 3), "solve_ms_group": round(t_grp, 3),
+            "remote_pairs": remote, "scatter_ms": round(scatter, 3),
+            "gather_ms_per_group": round(gather_grp, 3), "ms_per_pass": round(total, 3),
+            "pairs_per_s": round(pairs / total * 1e3, 1)}
+
+
+def chunk_costs(rows, cols, chunk, nchunks=12):
+    """GPU ms and host ms of one eager chunk on a rows x cols band."""
+    I0, I1 = hsflow.synth_pair(1000, rows, cols)
+    t0 = torch.from_numpy(I0).cuda().half()
+    t1 = torch.from_numpy(I1).cuda().half()
+    ws = hsflow.alloc_workspace(rows, cols, 1)
+    u = torch.zeros((rows, cols), dtype=torch.float32, device="cuda")
+    v = torch.zeros_like(u)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    k1 = time.perf_counter()
+    hsflow.gradients_device(t0, t1, ws)
+    torch.cuda.synchronize()
+    k1 = (time.perf_counter() - k1) * 1e3
+    for _ in range(3):
+        hsflow.jacobi_device(rows, cols, 1, 5, chunk, 1.0, u, v, ws, warm_start=True)
+    torch.cuda.synchronize()
+    host = []
+    e0.record()
+    for _ in range(nchunks):
+        h = time.perf_counter()
+        hsflow.jacobi_device(rows, cols, 1, 5, chunk, 1.0, u, v, ws, warm_start=True)
+        host.append((time.perf_counter() - h) * 1e3)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / nchunks, float(np.median(host)), k1
+
+
+def bands_prediction(n, chunk=12, iters=1000):
+    p = rb.plan(4320, 7680, 3, n, 5, chunk)
+    out = {"n": n, "chunk": chunk, "halo_rows": p.halo, "levels": []}
+    total = 0.0
+    for l in range(p.levels - 1, -1, -1):
+        R, C = p.sizes[l]
+        ext = max(b.e1 - b.e0 for b in p.bands[l])
+        g, h, k1 = chunk_costs(ext, C, chunk)
+        nch = -(-iters // chunk)
+        per_chunk = max(g + (XCHG_US / 1e3 if n > 1 else 0.0),
+                        h + (XCHG_HOST_US / 1e3 if n > 1 else 0.0))
+        lvl = nch * per_chunk + k1
+        total += lvl
+        out["levels"].append({"level": l, "band_rows": ext, "cols": C, "chunks": nch,
+                              "gpu_ms_per_chunk": round(g, 4), "host_ms_per_chunk": round(h, 4),
+                              "ms": round(lvl, 3)})
+    own = 4320 // n * 7680 * 8 / 1e6  # MB of (u, v) per remote rank
+    gather = own / LINK_GBPS if n > 1 else 0.0
+    total += gather
+    out["gather_ms"] = round(gather, 3)
+    out["ms_per_pair"] = round(total, 2)
+    return out
+
+
+def main():
+    res = {"constants": {"LINK_GBPS": LINK_GBPS, "XCHG_US": XCHG_US,
+                         "XCHG_HOST_US": XCHG_HOST_US},
+           "resident_1080p_x8_ms": round(resident_ms(8), 3)}
+    res["stream"] = [stream_prediction(n) for n in (1, 2, 4, 8)]
+    res["bands"] = [bands_prediction(n) for n in (1, 2, 4, 8)]
+    res["bands_chunk24"] = [bands_prediction(n, 24) for n in (2, 4, 8)]
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -275,7 +275,7 @@ def test_device_bands_graphed_bit_identical(hs, overlap):
     assert torch.equal(u, ur) and torch.equal(v, vr)
 
 
-def test_graphed_refuses_dist_comm_and_rank_streams():
+def test_graphed_refuses_dist_comm_and_overlapped_rank_streams():
     p = rb.plan(64, 30, 1, 2, 5, 2)
 
     class O:
@@ -284,4 +284,28 @@ def test_graphed_refuses_dist_comm_and_rank_streams():
     with pytest.raises(ValueError):
         rb.graphed(rb.solve, [None] * 2, [None] * 2, p, 4, [O(), O()], rb.DistComm(), [0, 1])
     with pytest.raises(ValueError):
-        rb.graphed(rb.solve, [None] * 2, [None] * 2, p, 4, [O(), O()], rb.LocalComm(), [0, 1])
+        rb.graphed(rb.solve_overlapped, [None] * 2, [None] * 2, p, 4, [O(), O()],
+                   rb.LocalComm(), [0, 1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlap", [False])
+def test_device_bands_graphed_with_rank_streams(hs, overlap):
+    """The capture round 3 fenced off: every virtual rank on a stream of its
+    own.  graphed() forks the rank streams from the capturing stream first,
+    so the whole plain schedule is captured; replays give the undivided
+    solve's bits.  (The overlapped schedule with rank streams still crashes
+    inside hipStreamEndCapture and is refused: DESIGN.md §6.)"""
+    I0, I1 = hs.synth_pair(1000, 400, 522)
+    t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
+    p = rb.plan(400, 522, 2, 3, 5, 6)
+    ops = [rb.DeviceOps(5, 1.0, t0.device, stream=torch.cuda.Stream()) for _ in range(3)]
+    solver = rb.solve_overlapped if overlap else rb.solve
+    g, u, v = rb.graphed(solver, [t0] * 3, [t1] * 3, p, 40, ops, rb.LocalComm(), [0, 1, 2])
+    u.fill_(float("nan"))
+    v.fill_(float("nan"))
+    g.replay()
+    g.replay()
+    ur, vr = hs.flow_pyramid_device(t0, t1, 2, 5, 40, 1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(u, ur) and torch.equal(v, vr)
