@@ -156,8 +156,11 @@ def parse(argv=None):
                          "(the metric, plus the secondary / e2e / stream legs); stream: "
                          "BASELINE config 4 alone; bands: BASELINE config 5 on N GPUs, "
                          "ONE pair split into row bands with a halo exchange")
-    ap.add_argument("--chunk", type=int, default=12,
-                    help="bands mode: iterations between halo exchanges")
+    ap.add_argument("--chunk", default="24,48",
+                    help="bands: iterations between halo exchanges, one value or one per "
+                         "pyramid level from the finest (the last repeats): coarse levels "
+                         "carry little work per chunk, so longer chunks there save "
+                         "exchanges")
     ap.add_argument("--overlap", action="store_true",
                     help="bands mode: hide each exchange behind the next chunk's interior "
                          "(row_bands.solve_overlapped; bit-identical)")
@@ -1075,7 +1078,8 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     window, alpha = args.window, args.alpha
     # one rank exchanges nothing: its band is the whole plane, solved in one
     # call per level
-    chunk = chunk or (args.chunk if world > 1 else iters)
+    if chunk is None:
+        chunk = ([int(x) for x in str(args.chunk).split(",")] if world > 1 else iters)
     tdt = {"f16": torch.float16, "f32": torch.float32, "u8": torch.uint8}[in_dtype]
     I0 = torch.empty((rows, cols), dtype=tdt, device=dev)
     I1 = torch.empty_like(I0)
@@ -1102,13 +1106,14 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     elapsed = timed_region(one, sync, steps, warmup, world, dev)
     px_all = sum(r * c for r, c in p.sizes)
-    exchanges = sum(-(-iters // chunk) for _ in range(levels)) if world > 1 else 0
+    exchanges = sum(-(-iters // c) for c in p.chunks) if world > 1 else 0
     leg = {"workload": f"{cols}x{rows} {in_dtype}, {levels} levels, {iters} it/level, "
                        f"ws {window}, one pair in {world} row band" + ("s" if world > 1 else ""),
            "value": round(px_all * iters * steps / elapsed / 1e6, 1), "unit": "Mpix*iter/s",
            "ms_per_pair": round(elapsed / steps * 1e3, 3), "steps": steps,
            "pairs_per_s": round(steps / elapsed, 2),
-           "n_ranks": world, "chunk": chunk, "halo_rows": p.halo,
+           "n_ranks": world, "chunks_per_level": list(p.chunks),
+           "halo_rows_per_level": list(p.halos),
            "exchanges_per_solve": exchanges,
            "exchange": "overlapped with interior iterations" if overlap else "after every chunk",
            "transport": _transport(world, dev), "scaling": "strong"}
@@ -1137,7 +1142,8 @@ def bands_mode(args, world, rank, dev):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic frame pair",
             "config": {"workload": leg["workload"], "window": args.window,
-                       "chunk": leg["chunk"], "halo_rows": leg["halo_rows"],
+                       "chunks_per_level": leg["chunks_per_level"],
+                       "halo_rows_per_level": leg["halo_rows_per_level"],
                        "exchange": leg["exchange"],
                        "parallelism": f"row bands x{world}"},
             "parity": leg["parity"], "bands": leg}), flush=True)

@@ -58,10 +58,12 @@ class Plan:
     levels: int
     world: int
     window: int
-    chunk: int
-    halo: int
+    chunk: int            # level 0's chunk (chunks[0])
+    halo: int             # level 0's halo (halos[0])
     sizes: tuple          # (rows_l, cols_l) per level
     bands: tuple          # bands[l][rank]
+    chunks: tuple = ()    # iterations between exchanges, per level
+    halos: tuple = ()     # halo rows, per level
 
 
 def anchors(window: int):
@@ -69,14 +71,42 @@ def anchors(window: int):
     return A, window - 1 - A
 
 
-def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk: int) -> Plan:
-    """Row bands for every level.  Raises ValueError if a band at some level
-    would be shorter than the halo (too many ranks for the image)."""
-    if world < 1 or levels < 1 or chunk < 1:
-        raise ValueError("world, levels and chunk must be >= 1")
+def level_chunks(chunk, levels: int) -> tuple:
+    """`chunk` as one int for every level, or a sequence from level 0
+    (finest) up, its last entry repeated for the coarser levels."""
+    if isinstance(chunk, int):
+        return (chunk,) * levels
+    c = tuple(int(x) for x in chunk)
+    if not c:
+        raise ValueError("empty chunk list")
+    return (c + (c[-1],) * levels)[:levels]
+
+
+def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk) -> Plan:
+    """Row bands for every level.  `chunk`: iterations between exchanges,
+    one int or one per level (level 0 first; coarse levels have little work
+    per chunk, so fewer, longer chunks there cut the exchanges the solve
+    waits on).  Raises ValueError if a band at some level would be shorter
+    than its halo (too many ranks for the image)."""
+    if world < 1 or levels < 1:
+        raise ValueError("world and levels must be >= 1")
+    chunks = level_chunks(chunk, levels)
+    if min(chunks) < 1:
+        raise ValueError("chunks must be >= 1")
     A, AR = anchors(window)
-    H = chunk * max(A, AR, 1)
-    H += H & 1                      # even: extended bands start on even rows
+    halos = []
+    for c in chunks:
+        H = c * max(A, AR, 1)
+        H += H & 1                  # even: extended bands start on even rows
+        halos.append(H)
+    # the warm start of level l reads the coarse rows [e0/2, (e1+1)/2) of its
+    # extended band, valid after level l+1's last exchange only if the coarse
+    # halo covers them
+    for l in range(levels - 1):
+        if world > 1 and halos[l + 1] < halos[l] // 2 + 1:
+            raise ValueError(f"level {l + 1}'s halo {halos[l + 1]} cannot cover level {l}'s "
+                             f"warm start (halo {halos[l]}): give coarser levels chunks at "
+                             "least half as long")
     # nested bands on every level, each starting on an even row (even at the
     # coarsest level): the Jacobi kernels add the vertical window sums in an
     # order fixed by image-row parity, so a band solved as its own plane
@@ -90,6 +120,7 @@ def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk: int)
                   for k in range(1, world)] + [rows]
     bands = []
     for l, (R, _) in enumerate(sizes):
+        H = halos[l]
         lv = []
         for r in range(world):
             a = cuts[r] >> l
@@ -100,7 +131,8 @@ def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk: int)
             lv.append(Band(a, b, max(0, a - H) if r > 0 else 0,
                            min(R, b + H) if r < world - 1 else R))
         bands.append(tuple(lv))
-    return Plan(rows, cols, levels, world, window, chunk, H, tuple(sizes), tuple(bands))
+    return Plan(rows, cols, levels, world, window, chunks[0], halos[0], tuple(sizes),
+                tuple(bands), chunks, tuple(halos))
 
 
 # --------------------------------------------------------------------- ops
@@ -213,7 +245,7 @@ class LocalComm:
     def start_strips(self, states: Sequence["RankState"]):
         """The overlapped schedule's exchange: each rank's send buffers into
         its neighbours' strip halo rows (one fused copy for all ranks)."""
-        H = states[0].plan.halo
+        H = states[0].strips.H
         d, x = [], []
         for up, dn in zip(states, states[1:]):
             su, sd = up.strips, dn.strips
@@ -246,7 +278,7 @@ class LocalComm:
 
     def _copy_halos(self, states: Sequence["RankState"], level: int):
         p = states[0].plan
-        H = p.halo
+        H = p.halos[level]
         for r in range(p.world - 1):
             up, dn = states[r], states[r + 1]
             bu, bd = p.bands[level][r], p.bands[level][r + 1]
@@ -272,7 +304,7 @@ class DistComm:
         import torch
         import torch.distributed as dist
         (s,) = states
-        p, r, H = s.plan, s.rank, s.plan.halo
+        p, r, H = s.plan, s.rank, s.plan.halos[level]
         band = p.bands[level][r]
         ops = []
 
@@ -295,7 +327,8 @@ class DistComm:
         import torch
         import torch.distributed as dist
         (s,) = states
-        p, r, H, st = s.plan, s.rank, s.plan.halo, s.strips
+        p, r, st = s.plan, s.rank, s.strips
+        H = st.H
         ops = []
 
         def t(x):
@@ -341,7 +374,7 @@ def solve(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
             handles.append(s.ops.gradients(s.P0[l][bd.e0:bd.e1], s.P1[l][bd.e0:bd.e1]))
         done = 0
         while True:
-            n = min(p.chunk, iters - done)
+            n = min(p.chunks[l], iters - done)
             if n > 0:
                 for s, h in zip(states, handles):  # each rank owns its ops/workspace
                     bd = p.bands[l][s.rank]
@@ -391,7 +424,8 @@ def _jacobi_stack(ops, g, U, V, n: int, side=False):
 def overlap_ok(p: Plan) -> bool:
     """The overlapped schedule needs every band to hold two halos of rows
     (its edge strips' valid rows and the interior's must tile the band)."""
-    return p.world > 1 and all(bd.b - bd.a >= 2 * p.halo for lv in p.bands for bd in lv)
+    return p.world > 1 and all(bd.b - bd.a >= 2 * p.halos[l]
+                               for l, lv in enumerate(p.bands) for bd in lv)
 
 
 class StripSet:
@@ -404,7 +438,7 @@ class StripSet:
     a send may still read them)."""
 
     def __init__(self, s: "RankState", l: int):
-        p, H = s.plan, s.plan.halo
+        p, H = s.plan, s.plan.halos[l]
         R, _ = p.sizes[l]
         bd = p.bands[l][s.rank]
         self.H, self.a, self.b = H, bd.a, bd.b
@@ -477,7 +511,7 @@ def strip_groups(states, l: int):
     out = []
     for grp in groups:
         ops = grp[0].ops
-        p, H = grp[0].plan, grp[0].plan.halo
+        p, H = grp[0].plan, grp[0].plan.halos[l]
         C = p.sizes[l][1]
         sets = [StripSet(s, l) for s in grp]
         n = sum(x.n for x in sets)
@@ -558,7 +592,7 @@ def solve_overlapped(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Seque
         pending = None
         done = 0
         while done < iters:
-            n = min(p.chunk, iters - done)
+            n = min(p.chunks[l], iters - done)
             first = done == 0
             copies(lambda s: s.strips.snapshot(s.u[l], s.v[l], with_halos=first))
             for s, g in zip(states, gi):
@@ -609,12 +643,6 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
     import torch
     if not isinstance(comm, LocalComm):
         raise ValueError("graphed(): LocalComm virtual ranks only")
-    if solver is solve_overlapped and any(getattr(o, "stream", None) is not None
-                                          for o in ops_list):
-        # measured: still crashes inside hipStreamEndCapture on this stack
-        # (scripts/lab/capture_bisect.py)
-        raise ValueError("graphed(): the overlapped schedule takes virtual ranks on the "
-                         "caller's stream only")
     dev = ops_list[0].device
     side = torch.cuda.Stream(device=dev)
     side.wait_stream(torch.cuda.current_stream(dev))
@@ -622,14 +650,30 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
         gather_owned(solver(I0s, I1s, p, iters, ops_list, comm, ranks), p, comm)
     torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize(dev)
+    rank_streams = any(getattr(o, "stream", None) is not None for o in ops_list)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
-        cap = torch.cuda.current_stream(dev)
-        for o in ops_list:  # fork every rank stream from the capture
-            if getattr(o, "stream", None) is not None:
-                o.stream.wait_stream(cap)
-        st = solver(I0s, I1s, p, iters, ops_list, comm, ranks)
-        u, v = gather_owned(st, p, comm)
+    import hsflow
+    if rank_streams:
+        # the library's side streams would be forked from a rank stream:
+        # keep every batch on its caller's stream during this capture
+        hsflow.set_max_streams(1)
+    try:
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            cap = torch.cuda.current_stream(dev)
+            # every stream the solve will use joins the capture from the
+            # capturing stream itself, before anything forks it from another
+            # stream: a stream whose first capture dependency is a non-origin
+            # capturing stream crashes hipStreamEndCapture on this stack
+            # (scripts/lab/capture_ops.py side2)
+            for o in ops_list:
+                for x in (getattr(o, "stream", None), getattr(o, "_side", None)):
+                    if x is not None:
+                        x.wait_stream(cap)
+            st = solver(I0s, I1s, p, iters, ops_list, comm, ranks)
+            u, v = gather_owned(st, p, comm)
+    finally:
+        if rank_streams:
+            hsflow.set_max_streams(0)
     return g, u, v
 
 

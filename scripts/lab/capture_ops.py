@@ -7,7 +7,10 @@ one does not; scripts/lab/capture_bisect.py).  One operation per process:
       stack    torch.stack of row views on the forked stream
       foreach  torch._foreach_copy_ of row views on the forked stream
       foreach_origin  the same copies on the capture's origin stream
-      side2    a third stream forked from the second and joined back
+      side2    a third stream forked from the second and joined back: CRASHES
+               inside hipStreamEndCapture (a stream whose first capture
+               dependency is a non-origin capturing stream)
+      side2_pre  the same, with the third stream first forked from the origin
 The capture forks stream B from the origin A, runs MODE's work on B, joins
 B back into A and ends the capture; then replays once and checks values."""
 import sys
@@ -23,6 +26,8 @@ def main(mode):
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=A, capture_error_mode="thread_local"):
+        if mode == "side2_pre":
+            C.wait_stream(A)  # C joins the capture through the origin first
         B.wait_stream(A)
         with torch.cuda.stream(B):
             if mode == "alloc":
@@ -33,7 +38,7 @@ def main(mode):
                 out.copy_(s)
             elif mode == "foreach":
                 torch._foreach_copy_([out[0], out[1]], [base[0:8], base[8:16]])
-            elif mode == "side2":
+            elif mode in ("side2", "side2_pre"):
                 C.wait_stream(B)
                 with torch.cuda.stream(C):
                     out[0].copy_(base[0:8])

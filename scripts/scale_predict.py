@@ -8,13 +8,14 @@ stream leg (configs[3]): 64 1080p pairs held by rank 0; rank r solves pairs
   r, r + N, ... in 2 groups (one at N = 1); rank 0 sends 2 x 8.3 MB of f32
   frames per pair to its owner and receives 2 x 8.3 MB of (u, v) back.
   Measured: the resident solve time of a 64/N-pair batch and of half of it.
-  Modelled: rank 0 sends the remote pairs over N - 1 links in parallel at
-  LINK_GBPS each (RCCL point-to-point over xGMI), the gather likewise; the
-  scatter precedes the first solve, group 0's gather overlaps group 1's
-  solve, group 1's gather is exposed.
+  Modelled: rank 0 sends a group to every rank at once (one batch per
+  group), each link at LINK_GBPS (RCCL point-to-point over xGMI); group c+1
+  travels while group c is solved, group c's (u, v) return while group c+1
+  is solved, the last group's return is exposed.
 bands leg (configs[4] as stated for N GPUs): one 8K fp16 pair, 3 levels x
-  1000 it, rank r solves its extended band in chunks of `chunk` iterations
-  with a halo exchange after each.  Measured: per level, the GPU time and
+  1000 it, rank r solves its extended band in chunks (24 iterations at level
+  0, 48 at the coarser levels: bench.py's default) with a halo exchange
+  after each.  Measured: per level, the GPU time and
   the host issue time of one chunk on the largest extended band (eager
   jacobi_device calls, as row_bands.solve issues them), K1 per level, the
   pyramid build.  Modelled: an exchange costs XCHG_US of latency on the
@@ -69,13 +70,20 @@ def stream_prediction(n, pairs=64):
     t_grp = resident_ms(max(1, per // groups)) if groups > 1 else t_all
     mb = 2 * 1080 * 1920 * 4 / 1e6  # one direction, one pair
     remote = pairs - per             # pairs rank 0 does not own
-    # rank 0 feeds n - 1 links at once; per link: per pairs
-    scatter = per * mb / LINK_GBPS if n > 1 else 0.0
-    gather_grp = (per // groups) * mb / LINK_GBPS if n > 1 else 0.0
+    # rank 0 sends each group to every rank at once (one batch per group,
+    # frame_parallel.run_stream_pipelined): a group crosses each link in
+    # per/groups pairs' time; group c+1 travels while group c is solved;
+    # group c's (u, v) return while group c+1 is solved
+    grp_link = (per // groups) * mb / LINK_GBPS if n > 1 else 0.0
+    scatter = grp_link * groups
+    gather_grp = grp_link
     if n == 1:
         total = t_all
     else:
-        total = scatter + t_grp + max(t_grp, gather_grp) + gather_grp
+        t = grp_link                          # group 0 arrived
+        for c in range(groups):
+            t = max(t, (c + 1) * grp_link) + t_grp  # group c solved
+        total = t + gather_grp                # the last group's (u, v) home
     return {"n": n, "pairs_per_rank": per, "groups": groups,
             "solve_ms_rank_share": round(t_all, 3), "solve_ms_group": round(t_grp, 3),
             "remote_pairs": remote, "scatter_ms": round(scatter, 3),
@@ -111,15 +119,17 @@ def chunk_costs(rows, cols, chunk, nchunks=12):
     return e0.elapsed_time(e1) / nchunks, float(np.median(host)), k1
 
 
-def bands_prediction(n, chunk=12, iters=1000):
-    p = rb.plan(4320, 7680, 3, n, 5, chunk)
-    out = {"n": n, "chunk": chunk, "halo_rows": p.halo, "levels": []}
+def bands_prediction(n, chunk=(24, 48), iters=1000):
+    p = rb.plan(4320, 7680, 3, n, 5, chunk if n > 1 else iters)
+    out = {"n": n, "chunks_per_level": list(p.chunks), "halo_rows_per_level": list(p.halos),
+           "levels": []}
     total = 0.0
     for l in range(p.levels - 1, -1, -1):
         R, C = p.sizes[l]
         ext = max(b.e1 - b.e0 for b in p.bands[l])
-        g, h, k1 = chunk_costs(ext, C, chunk)
-        nch = -(-iters // chunk)
+        ck = p.chunks[l]
+        g, h, k1 = chunk_costs(ext, C, ck)
+        nch = -(-iters // ck)
         per_chunk = max(g + (XCHG_US / 1e3 if n > 1 else 0.0),
                         h + (XCHG_HOST_US / 1e3 if n > 1 else 0.0))
         lvl = nch * per_chunk + k1
@@ -141,7 +151,7 @@ def main():
            "resident_1080p_x8_ms": round(resident_ms(8), 3)}
     res["stream"] = [stream_prediction(n) for n in (1, 2, 4, 8)]
     res["bands"] = [bands_prediction(n) for n in (1, 2, 4, 8)]
-    res["bands_chunk24"] = [bands_prediction(n, 24) for n in (2, 4, 8)]
+    res["bands_chunk12"] = [bands_prediction(n, 12) for n in (2, 4, 8)]
     print(json.dumps(res, indent=1))
 
 

@@ -151,6 +151,7 @@ def test_bench_bands_leg_over_gloo(overlap):
     assert isinstance(leg0, dict) and isinstance(leg1, dict), (leg0, leg1)
     assert leg0["n_ranks"] == 2 and leg0["transport"] == "gloo (cpu tensors)"
     assert leg0["exchanges_per_solve"] == B_LEVELS * -(-B_ITERS // B_CHUNK)
+    assert leg0["chunks_per_level"] == [B_CHUNK] * B_LEVELS
     assert leg0["ms_per_pair"] == leg1["ms_per_pair"] > 0  # max over ranks
     assert leg0["parity"]["ok"] is None  # no committed golden at this size
     I0, I1 = synth_pair(1000, B_ROWS, B_COLS)

@@ -86,7 +86,8 @@ def _pair(rows, cols, seed=1000):
 
 
 @pytest.mark.parametrize("world,levels,chunk,window", [(2, 2, 3, 5), (3, 3, 2, 5),
-                                                       (4, 1, 2, 3)])
+                                                       (4, 1, 2, 3), (2, 3, (2, 4), 5),
+                                                       (3, 2, (1, 3), 5)])
 def test_local_bands_equal_undivided_oracle(world, levels, chunk, window):
     I0, I1 = _pair(70, 53)
     iters = 7
@@ -100,7 +101,8 @@ def test_local_bands_equal_undivided_oracle(world, levels, chunk, window):
 
 
 @pytest.mark.parametrize("world,levels,chunk,window,iters", [(2, 2, 3, 5, 7), (3, 1, 2, 5, 9),
-                                                             (4, 2, 2, 3, 5), (2, 1, 3, 5, 3)])
+                                                             (4, 2, 2, 3, 5), (2, 1, 3, 5, 3),
+                                                             (2, 2, (2, 3), 5, 7)])
 def test_local_overlapped_bands_equal_undivided_oracle(world, levels, chunk, window, iters):
     """The overlapped schedule (interior solved while the halos travel,
     edge strips solved from the received halos and a snapshot) gives the
@@ -115,6 +117,21 @@ def test_local_overlapped_bands_equal_undivided_oracle(world, levels, chunk, win
     u, v = rb.gather_owned(states, p, comm)
     uo, vo = oracle.flow_pyramid(I0, I1, levels, window, iters, 1.0)
     assert np.array_equal(u, uo) and np.array_equal(v, vo)
+
+
+def test_plan_per_level_chunks():
+    """Longer chunks on coarse levels (the bench's 24 / 48): one halo per
+    level; a coarse halo shorter than half the finer one is refused (the
+    finer level's warm start reads coarse halo rows)."""
+    p = rb.plan(4320, 7680, 3, 8, 5, (24, 48))
+    assert p.chunks == (24, 48, 48) and p.halos == (48, 96, 96)
+    assert p.chunk == 24 and p.halo == 48
+    for l, lv in enumerate(p.bands):
+        for k, bd in enumerate(lv):
+            assert bd.e0 == (0 if k == 0 else bd.a - p.halos[l])
+    with pytest.raises(ValueError):
+        rb.plan(400, 60, 2, 2, 5, (24, 4))
+    assert rb.level_chunks(7, 3) == (7, 7, 7)
 
 
 def test_overlap_needs_two_halos_per_band():
@@ -149,7 +166,7 @@ def _free_port():
 ROWS, COLS, LEVELS, ITERS, CHUNK = 104, 45, 2, 8, 3
 
 
-def _worker(rank, world, port, q, overlap=False):
+def _worker(rank, world, port, q, overlap=False, chunk=CHUNK):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
@@ -158,7 +175,7 @@ def _worker(rank, world, port, q, overlap=False):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         I0, I1 = synth_pair(1000, ROWS, COLS)
-        p = rb.plan(ROWS, COLS, LEVELS, world, 5, CHUNK)
+        p = rb.plan(ROWS, COLS, LEVELS, world, 5, chunk)
         comm = rb.DistComm()
         solve = rb.solve_overlapped if overlap else rb.solve
         states = solve([I0], [I1], p, ITERS, [OracleOps(5, 1.0)], comm, [rank])
@@ -170,15 +187,17 @@ def _worker(rank, world, port, q, overlap=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,overlap", [(2, False), (3, False), (2, True), (3, True)])
-def test_gloo_bands_equal_undivided_oracle(world, overlap):
+@pytest.mark.parametrize("world,overlap,chunk", [(2, False, CHUNK), (3, False, CHUNK),
+                                                 (2, True, CHUNK), (3, True, CHUNK),
+                                                 (3, False, (2, 4))])
+def test_gloo_bands_equal_undivided_oracle(world, overlap, chunk):
     """Plain and overlapped schedules over torch.distributed point-to-point
     (the code RCCL runs): the posted-then-waited exchange, send copies and
     all, gives the undivided solve's bits."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, overlap))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, overlap, chunk))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -275,7 +294,7 @@ def test_device_bands_graphed_bit_identical(hs, overlap):
     assert torch.equal(u, ur) and torch.equal(v, vr)
 
 
-def test_graphed_refuses_dist_comm_and_overlapped_rank_streams():
+def test_graphed_refuses_dist_comm():
     p = rb.plan(64, 30, 1, 2, 5, 2)
 
     class O:
@@ -283,19 +302,18 @@ def test_graphed_refuses_dist_comm_and_overlapped_rank_streams():
         device = "cpu"
     with pytest.raises(ValueError):
         rb.graphed(rb.solve, [None] * 2, [None] * 2, p, 4, [O(), O()], rb.DistComm(), [0, 1])
-    with pytest.raises(ValueError):
-        rb.graphed(rb.solve_overlapped, [None] * 2, [None] * 2, p, 4, [O(), O()],
-                   rb.LocalComm(), [0, 1])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("overlap", [False])
+@pytest.mark.parametrize("overlap", [False, True])
 def test_device_bands_graphed_with_rank_streams(hs, overlap):
     """The capture round 3 fenced off: every virtual rank on a stream of its
-    own.  graphed() forks the rank streams from the capturing stream first,
-    so the whole plain schedule is captured; replays give the undivided
-    solve's bits.  (The overlapped schedule with rank streams still crashes
-    inside hipStreamEndCapture and is refused: DESIGN.md §6.)"""
+    own (the overlapped schedule also forks a side stream per rank from its
+    rank stream).  graphed() joins every one of those streams to the capture
+    from the capturing stream first -- a stream whose first capture
+    dependency is another non-origin stream crashes hipStreamEndCapture
+    (scripts/lab/capture_ops.py) -- so the whole schedule is captured;
+    replays give the undivided solve's bits."""
     I0, I1 = hs.synth_pair(1000, 400, 522)
     t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
     p = rb.plan(400, 522, 2, 3, 5, 6)
