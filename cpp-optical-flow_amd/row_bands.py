@@ -207,21 +207,30 @@ class DeviceOps:
         self.hs.gradients_device(J0, J1, ws, stream=self.stream)
         return ws
 
+    # flat: no side stream (set by graphed() while it captures rank streams:
+    # a stream forked from a non-origin capturing stream crashes
+    # hipStreamEndCapture on this ROCm stack, scripts/lab/capture_ops.py)
+    flat = False
+
     def jacobi_stack(self, ws, U, V, n: int, side: bool = False):
         b, r, c = U.shape
+        st = self._side if (side and not self.flat) else self.stream
         self.hs.jacobi_device(r, c, b, self.window, n, self.alpha, U, V, ws,
-                              warm_start=True, stream=self._side if side else self.stream)
+                              warm_start=True, stream=st)
 
     def _main(self):
         return self.torch.cuda.current_stream(self.device) if self.stream is None else self.stream
 
     def fork(self):
+        if self.flat:
+            return
         if not hasattr(self, "_side"):
             self._side = self.torch.cuda.Stream(device=self.device)
         self._side.wait_stream(self._main())
 
     def join(self):
-        self._main().wait_stream(self._side)
+        if not self.flat:
+            self._main().wait_stream(self._side)
 
 
 # -------------------------------------------------------------------- comm
@@ -654,26 +663,32 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
     g = torch.cuda.CUDAGraph()
     import hsflow
     if rank_streams:
-        # the library's side streams would be forked from a rank stream:
-        # keep every batch on its caller's stream during this capture
+        # Inside a capture, a stream forked from a capturing stream that is
+        # not the capture's origin -- here: a rank stream's side stream, or
+        # the library's split streams under a rank stream -- crashes
+        # hipStreamEndCapture (ROCm 7.2; reproducer scripts/lab/capture_ops.py
+        # side2, also when the side stream joined the capture from the origin
+        # first: side2_pre).  So while capturing, every rank keeps its work
+        # on its own stream (the ranks' streams still run side by side), and
+        # the library does not split batches.
         hsflow.set_max_streams(1)
+        for o in ops_list:
+            if hasattr(o, "flat"):
+                o.flat = True
     try:
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             cap = torch.cuda.current_stream(dev)
-            # every stream the solve will use joins the capture from the
-            # capturing stream itself, before anything forks it from another
-            # stream: a stream whose first capture dependency is a non-origin
-            # capturing stream crashes hipStreamEndCapture on this stack
-            # (scripts/lab/capture_ops.py side2)
-            for o in ops_list:
-                for x in (getattr(o, "stream", None), getattr(o, "_side", None)):
-                    if x is not None:
-                        x.wait_stream(cap)
+            for o in ops_list:  # every rank stream forked from the origin
+                if getattr(o, "stream", None) is not None:
+                    o.stream.wait_stream(cap)
             st = solver(I0s, I1s, p, iters, ops_list, comm, ranks)
             u, v = gather_owned(st, p, comm)
     finally:
         if rank_streams:
             hsflow.set_max_streams(0)
+            for o in ops_list:
+                if hasattr(o, "flat"):
+                    o.flat = False
     return g, u, v
 
 

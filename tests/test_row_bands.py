@@ -308,12 +308,11 @@ def test_graphed_refuses_dist_comm():
 @pytest.mark.parametrize("overlap", [False, True])
 def test_device_bands_graphed_with_rank_streams(hs, overlap):
     """The capture round 3 fenced off: every virtual rank on a stream of its
-    own (the overlapped schedule also forks a side stream per rank from its
-    rank stream).  graphed() joins every one of those streams to the capture
-    from the capturing stream first -- a stream whose first capture
-    dependency is another non-origin stream crashes hipStreamEndCapture
-    (scripts/lab/capture_ops.py) -- so the whole schedule is captured;
-    replays give the undivided solve's bits."""
+    own.  graphed() forks the rank streams from the capturing stream and,
+    while capturing, keeps each rank's work on its rank stream (a stream
+    forked from a non-origin capturing stream crashes hipStreamEndCapture on
+    ROCm 7.2: scripts/lab/capture_ops.py side2); the whole schedule is
+    captured and replays give the undivided solve's bits."""
     I0, I1 = hs.synth_pair(1000, 400, 522)
     t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
     p = rb.plan(400, 522, 2, 3, 5, 6)
