@@ -788,10 +788,13 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
         stream = [tuple(torch.from_numpy(a).to(dev) for a in
                         hsflow.synth_pair(1000 + j, rows, cols)) for j in range(n)]
     mine = fp.my_pairs(n, rank, world)
-    # N > 1: each rank's share in 2 groups, so group 0's (u, v) travel back
-    # while group 1 is solved (frame_parallel.run_stream_pipelined); one
-    # rank has nothing to overlap and solves its share in one call
-    chunks = 2 if world > 1 else 1
+    # N > 1: each rank's share in groups of at most 8 pairs (at least 2), so
+    # group c+1 travels while group c is solved and group c's (u, v) travel
+    # back while group c+1 is solved (frame_parallel.run_stream_pipelined;
+    # 8 pairs fill the chip, smaller groups start sooner:
+    # scripts/scale_predict.py); one rank has nothing to overlap and solves
+    # its share in one call
+    chunks = max(2, -(-len(mine) // 8)) if world > 1 else 1
     if solve_batch is None:
         ws = hsflow.alloc_workspace(rows, cols, max(1, -(-len(mine) // chunks)), dev)
 

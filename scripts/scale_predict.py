@@ -7,7 +7,8 @@ runs are the driver's; DESIGN.md §6 "Predictions" quotes this output).
 stream leg (configs[3]): 64 1080p pairs held by rank 0; rank r solves pairs
   r, r + N, ... in 2 groups (one at N = 1); rank 0 sends 2 x 8.3 MB of f32
   frames per pair to its owner and receives 2 x 8.3 MB of (u, v) back.
-  Measured: the resident solve time of a 64/N-pair batch and of half of it.
+  A rank's share goes in groups of <= 8 pairs (at least 2; bench.stream_leg).
+  Measured: the resident solve time of a 64/N-pair batch and of one group.
   Modelled: rank 0 sends a group to every rank at once (one batch per
   group), each link at LINK_GBPS (RCCL point-to-point over xGMI); group c+1
   travels while group c is solved, group c's (u, v) return while group c+1
@@ -65,7 +66,7 @@ def resident_ms(batch, reps=6):
 
 def stream_prediction(n, pairs=64):
     per = pairs // n
-    groups = 2 if n > 1 else 1
+    groups = max(2, -(-per // 8)) if n > 1 else 1  # bench.stream_leg
     t_all = resident_ms(per)
     t_grp = resident_ms(max(1, per // groups)) if groups > 1 else t_all
     mb = 2 * 1080 * 1920 * 4 / 1e6  # one direction, one pair
