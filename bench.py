@@ -273,6 +273,14 @@ def parity_check(u, v, golden):
 
 # --------------------------------------------------------------- timing
 PREWARM_S = 0.15
+_T0 = time.perf_counter()
+
+
+def progress(msg, rank=0):
+    """One stderr line per leg (the GPU pool takes a command that prints
+    nothing for 3 minutes for hung); stdout keeps the one JSON line."""
+    print(f"bench [rank {rank}, {time.perf_counter() - _T0:6.1f} s]: {msg}", file=sys.stderr,
+          flush=True)
 
 
 def prewarm(step, sync, seconds=PREWARM_S, max_steps=400):
@@ -919,6 +927,7 @@ def main():
     if args.kb:
         hsflow.set_iters_per_launch(args.kb)
     keep = default_run and not args.no_stream
+    progress(f"resident {args.workload}", rank)
     prim = resident_leg(args.workload, args, dev, world, rank, init_dist, keep=keep)
     resident_ref = None
     if keep:
@@ -926,15 +935,19 @@ def main():
     sec = c5 = w3 = None
     singles = {}
     if default_run and not args.no_secondary:
+        progress("resident 4k", rank)
         sec = resident_leg("4k", args, dev, world, rank)
     if default_run and not args.no_w3:
         # windowSize 5 is the headline, report 3 (north_star) too
+        progress("resident 1080p w3", rank)
         w3 = resident_leg("1080p", args, dev, world, rank, window=3)
     if default_run and not args.no_8k:
+        progress("resident 8k pyramid", rank)
         c5 = resident_leg("8k", args, dev, world, rank)
     if default_run and not args.no_single:
         # configs[1] / configs[2] as stated: one pair per solve (main.cpp:97-98)
         for wl in ("1080p", "4k"):
+            progress(f"single pair {wl}", rank)
             singles[wl] = resident_leg(wl, args, dev, world, rank, batch=1)
     stream_peak = hbm_stream_peak(dev) if rank == 0 else None
     e2e = None
@@ -943,6 +956,7 @@ def main():
     strm = None
     if default_run and not args.no_stream:
         golden = golden_entry(1080, 1920, 300, 5, 1, 1.0) if rank == 0 else None
+        progress("stream (configs[3])", rank)
         strm = stream_leg("1080p", args, world, rank, dev, ref=resident_ref, golden=golden)
     del resident_ref
     bands = None
@@ -950,12 +964,16 @@ def main():
         # BASELINE configs[4] as stated for N GPUs: one 8K pair in N row
         # bands, halo rows over RCCL (at N = 1: one band, no exchange)
         init_dist()
+        progress("bands (configs[4])", rank)
         bands = bands_leg(args, world, rank, dev, steps=max(1, min(args.steps, 5)), warmup=1)
 
+    if default_run and rank == 0:
+        progress("config1 + host_api", rank)
     c1 = config1_leg(dev) if (default_run and rank == 0) else None
     host_api = host_api_leg() if (default_run and rank == 0 and not args.no_host_api) else None
     cpu = cpu_all = None
     if rank == 0 and not args.no_cpu_baseline:
+        progress("cpu baseline", rank)
         # on every line, N > 1 included: the host-core figure the GPU counts
         # are read against (north_star)
         cpu = cpu_baseline(prim["rows"], prim["cols"], args.window, args.alpha,
