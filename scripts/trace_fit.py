@@ -11,8 +11,10 @@ single-stream Jacobi passes).  Every solve starts with one gradient launch
 (hs_gradients_kernel), so the trace splits into solves at those launches; the
 K solves just before the roofline group are the timed steps.  For each, the
 GPU span (first start to last end) and the busy time (union of kernel
-intervals) are printed next to the bench's ms_per_step, and the roofline
-group's mean Jacobi launch next to roofline.avg_launch_ms."""
+intervals) are printed next to the bench's ms_per_step, the Jacobi kernels'
+busy time per pass next to roofline.avg_launch_ms (the timed step's wall per
+pass), and the roofline group's mean single-stream launch next to
+roofline.isolated_launch.avg_launch_ms."""
 import csv
 import glob
 import json
@@ -59,10 +61,23 @@ def main():
            "busy_ms": [round(busy(g) / 1e6, 3) for g in timed],
            "span_ms_median": round(statistics.median(spans) / 1e6, 3)}
     res["span_over_bench_step"] = round(res["span_ms_median"] / b["ms_per_step"], 4)
+    roof = b.get("roofline") or {}
+    # the timed step's Jacobi kernels: busy time (union of the overlapping
+    # half-batch launches) per pass against the bench's top-level
+    # avg_launch_ms (= ms_per_step / passes)
+    passes = roof.get("launches_per_solve")
+    jbusy = [busy([k for k in g if k[2].startswith("hs_jacobi")]) for g in timed]
+    res["timed_jacobi_busy_ms"] = [round(x / 1e6, 3) for x in jbusy]
+    if passes:
+        res["timed_jacobi_busy_ms_per_pass_median"] = round(
+            statistics.median(jbusy) / 1e6 / passes, 5)
+        res["roofline_avg_launch_ms_bench"] = roof.get("avg_launch_ms")
+        res["trace_over_bench_per_pass"] = round(
+            res["timed_jacobi_busy_ms_per_pass_median"] / roof["avg_launch_ms"], 4)
     jac = [e - s for s, e, n in groups[roof_i] if n.startswith("hs_jacobi")]
-    res["roofline_group_launches"] = len(jac)
-    res["roofline_mean_launch_ms_trace"] = round(statistics.mean(jac) / 1e6, 5)
-    res["roofline_avg_launch_ms_bench"] = (b.get("roofline") or {}).get("avg_launch_ms")
+    res["isolated_group_launches"] = len(jac)
+    res["isolated_mean_launch_ms_trace"] = round(statistics.mean(jac) / 1e6, 5)
+    res["isolated_avg_launch_ms_bench"] = (roof.get("isolated_launch") or {}).get("avg_launch_ms")
     print(json.dumps(res, indent=1))
 
 
