@@ -353,7 +353,7 @@ def kernel_source_md5():
     return h.hexdigest()
 
 
-def pmc_for(wl_name, window, batch, kb, kernel, timed=False):
+def pmc_for(wl_name, window, batch, kb, kernel, timed=False, passes=None):
     """Committed PMC summary of this roofline leg (profiles/pmc_r04.json,
     written by scripts/pmc_collect.py from separate rocprofv3 --pmc passes)
     if it was collected for this kernel, blocking depth, batch and kernel
@@ -365,7 +365,8 @@ def pmc_for(wl_name, window, batch, kb, kernel, timed=False):
     with open(PMC_JSON) as f:
         e = json.load(f).get(("step_" if timed else "") + pmc_key(wl_name, window, batch))
     if e and e.get("kb") == kb and e.get("kernel") == kernel and \
-            e.get("kernel_source_md5") == kernel_source_md5():
+            e.get("kernel_source_md5") == kernel_source_md5() and \
+            (passes is None or e.get("passes_per_solve") == passes):
         return e
     return None
 
@@ -453,7 +454,8 @@ def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
                                       launches_per_solve / (pass_ms * 1e-3) / 1e9 /
                                       HBM_PEAK_GBPS, 4),
             "isolated_launch": iso}
-    tp = pmc_for(wl_name, window, batch, kb, kernel, timed=True) if step_ms else None
+    tp = (pmc_for(wl_name, window, batch, kb, kernel, timed=True, passes=launches_per_solve)
+          if step_ms else None)
     if tp is not None and tp.get("hbm_bytes_per_step"):
         per_pass = tp["hbm_bytes_per_step"] / launches_per_solve
         roof["traffic"] = int(per_pass)

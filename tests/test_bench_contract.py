@@ -157,3 +157,22 @@ def test_pmc_profile_used_only_for_the_kernel_source_it_was_collected_on(tmp_pat
     assert bench.pmc_for("1080p", 5, 8, 6, "hs_jacobi_wg_kernel") is None
     p.write_text(json.dumps({"1080p_w5_b8": dict(e, kernel_source_md5="0" * 32)}))
     assert bench.pmc_for("1080p", 5, 8, 6, "hs_jacobi_strip_kernel") is None
+
+
+def test_committed_pmc_profile_matches_the_kernel_sources():
+    """profiles/pmc_r04.json (what the bench's roofline reads) was collected
+    on the current Jacobi kernel sources, for the timed step of the headline
+    and 4K legs as well as the single-stream launches; its timed-step bytes
+    per pass are physical (the step's HBM traffic within 1.3x the
+    algorithmic bytes of its passes)."""
+    import bench
+    d = json.load(open(bench.PMC_JSON))
+    md5 = bench.kernel_source_md5()
+    for leg in ("1080p_w5_b8", "4k_w5_b2", "step_1080p_w5_b8", "step_4k_w5_b2"):
+        assert d[leg]["kernel_source_md5"] == md5, leg
+    for leg, (rows, cols, batch, passes) in {"step_1080p_w5_b8": (1080, 1920, 8, 50),
+                                             "step_4k_w5_b2": (2160, 3840, 2, 84)}.items():
+        e = d[leg]
+        assert e["passes_per_solve"] == passes and e["kb"] == 6
+        alg = rows * cols * batch * bench.PASS_BYTES_PER_PX
+        assert 1.0 <= e["hbm_bytes_per_step"] / passes / alg <= 1.3, leg
