@@ -309,7 +309,8 @@ class DistComm:
 
     def start(self, states: Sequence["RankState"], level: int):
         """Post the halo exchange; returns the requests (wait() completes
-        them: a stream wait under RCCL, a host wait under gloo)."""
+        them: a stream wait under RCCL, a host wait under gloo).  The sends
+        read the band itself: wait before the band's rows change."""
         import torch
         import torch.distributed as dist
         (s,) = states
@@ -319,14 +320,16 @@ class DistComm:
 
         def t(x):
             return torch.from_numpy(x) if isinstance(x, np.ndarray) else x
-        # send copies: the overlapped schedule rewrites the owned rows (its
-        # next interior solve) while a send may still be reading them
+        # the rows go straight from the band: exchange() waits for these
+        # requests before the next chunk rewrites them (under RCCL the wait
+        # orders the compute stream after the transfer), so no send copies
+        # (the overlapped schedule sends its own buffers, start_strips)
         for f in (s.u[level], s.v[level]):
             if r > 0:
-                ops.append(dist.P2POp(dist.isend, t(f[band.a:band.a + H]).clone(), r - 1))
+                ops.append(dist.P2POp(dist.isend, t(f[band.a:band.a + H]), r - 1))
                 ops.append(dist.P2POp(dist.irecv, t(f[band.a - H:band.a]), r - 1))
             if r < p.world - 1:
-                ops.append(dist.P2POp(dist.isend, t(f[band.b - H:band.b]).clone(), r + 1))
+                ops.append(dist.P2POp(dist.isend, t(f[band.b - H:band.b]), r + 1))
                 ops.append(dist.P2POp(dist.irecv, t(f[band.b:band.b + H]), r + 1))
         return dist.batch_isend_irecv(ops) if ops else []
 
