@@ -18,6 +18,6 @@ echo "bench wall seconds: $((SECONDS - t0))" | tee gpurun_out/bench_wall.txt
 cat gpurun_out/bench_default.json
 [ "$1" = "--trace" ] || exit 0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/bench_trace -o run --output-format csv -- \
-    python3 bench.py --no-secondary --no-w3 --no-8k --no-single --no-e2e --no-stream --no-cpu-baseline \
+    python3 bench.py --no-secondary --no-w3 --no-8k --no-single --no-e2e --no-stream --no-cpu-baseline --no-bands --no-host-api \
     > gpurun_out/bench_trace.json 2> gpurun_out/bench_trace.err || { echo "trace failed"; exit 1; }
 python3 scripts/trace_fit.py gpurun_out/bench_trace gpurun_out/bench_trace.json

@@ -2,7 +2,7 @@
 
     rocprofv3 --kernel-trace --stats -d gpurun_out/bench_trace -o run \
         --output-format csv -- python3 bench.py --no-secondary --no-w3 --no-8k \
-        --no-single --no-e2e --no-stream --no-cpu-baseline > gpurun_out/bench_trace.json
+        --no-single --no-e2e --no-stream --no-cpu-baseline --no-bands --no-host-api > gpurun_out/bench_trace.json
     python scripts/trace_fit.py gpurun_out/bench_trace gpurun_out/bench_trace.json
 
 The primary leg runs: one eager solve, a capture (no kernels execute), W
