@@ -27,6 +27,25 @@ s_h2d, s_cmp, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
 ev = {k: [torch.cuda.Event() for _ in range(2)] for k in ("in", "done", "in_free", "out_free")}
 
 
+# each slot's solve as one hipGraph, as bench.e2e_leg replays it
+graphs = []
+cur = torch.cuda.current_stream(dev)
+for sl in range(2):
+    cap = torch.cuda.Stream(dev)
+    cap.wait_stream(cur)
+    with torch.cuda.stream(cap):
+        hsflow.flow_device(d_in[sl][0], d_in[sl][1], 5, iters, 1.0, d_out[sl][0], d_out[sl][1],
+                           ws[sl], cap)
+    cur.wait_stream(cap)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        hsflow.flow_device(d_in[sl][0], d_in[sl][1], 5, iters, 1.0, d_out[sl][0], d_out[sl][1],
+                           ws[sl], torch.cuda.current_stream(dev))
+    graphs.append(g)
+torch.cuda.synchronize(dev)
+
+
 def run(n, h2d=True, d2h=True, solve=True, kd2h=False):
     for k in range(n):
         sl = k % 2
@@ -43,8 +62,7 @@ def run(n, h2d=True, d2h=True, solve=True, kd2h=False):
             if k >= 2:
                 s_cmp.wait_event(ev["out_free"][sl])
             if solve:
-                hsflow.flow_device(d_in[sl][0], d_in[sl][1], 5, iters, 1.0, d_out[sl][0],
-                                   d_out[sl][1], ws[sl], s_cmp)
+                graphs[sl].replay()
             ev["in_free"][sl].record(s_cmp)
             ev["done"][sl].record(s_cmp)
         with torch.cuda.stream(s_d2h):
