@@ -134,6 +134,27 @@ int main(int argc, char **argv) {
             CK(hipEventSynchronize(ev[k - 1]));
         }));
     }
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    std::printf("down 2 planes on 2 streams -> pinned   %.3f ms\n", med([&] {
+        CK(hipMemcpy2DAsync(pst, rb, dU, rb, rb, rows, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpy2DAsync(pst + n, rb, dU + n, rb, rb, rows, hipMemcpyDeviceToHost, s2));
+        CK(hipStreamSynchronize(s));
+        CK(hipStreamSynchronize(s2));
+    }));
+    std::printf("down 2 planes on 2 streams -> pageable %.3f ms\n", med([&] {
+        CK(hipMemcpy2DAsync(pagef.data(), rb, dU, rb, rb, rows, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpy2DAsync(pagef.data() + n, rb, dU + n, rb, rb, rows, hipMemcpyDeviceToHost,
+                            s2));
+        CK(hipStreamSynchronize(s));
+        CK(hipStreamSynchronize(s2));
+    }));
+    std::printf("up pageable 2 frames on 2 streams      %.3f ms\n", med([&] {
+        CK(hipMemcpyAsync(dI, f0.data(), n, hipMemcpyHostToDevice, s));
+        CK(hipMemcpyAsync(dI + n, f1.data(), n, hipMemcpyHostToDevice, s2));
+        CK(hipStreamSynchronize(s));
+        CK(hipStreamSynchronize(s2));
+    }));
     std::printf("down flat 2x -> pageable f32           %.3f ms\n", med([&] {
         CK(hipMemcpyAsync(pagef.data(), dU, n * 4, hipMemcpyDeviceToHost, s));
         CK(hipMemcpyAsync(pagef.data() + n, dU + n, n * 4, hipMemcpyDeviceToHost, s));
