@@ -655,7 +655,7 @@ def config1_leg(dev, reps=20):
 
 
 # --------------------------------------------------------------- e2e
-def e2e_leg(wl_name, args, dev, n_batches=12):
+def e2e_leg(wl_name, args, dev, n_batches=48):
     """End-to-end pairs/s as BASELINE.md defines it: pinned host u8 gray
     frames (what main.cpp:13-14 hands over) -> H2D -> K1 + K2 -> D2H of u, v
     (f32), batch after batch.  Copies run on their own streams and overlap
@@ -663,7 +663,12 @@ def e2e_leg(wl_name, args, dev, n_batches=12):
     downloads go through hsflow_download_device (the runtime's DMA engines):
     torch's copy_ into pinned memory runs as a 256-workgroup blit kernel per
     plane that takes the next batch's Jacobi workgroup slots (1275 vs ~1600
-    pairs/s; scripts/e2e_probe.py, scripts/pcie/d2h_engine_probe.hip)."""
+    pairs/s; scripts/e2e_probe.py, scripts/pcie/d2h_engine_probe.hip).
+    A stream of n_batches batches (384 pairs): the pipeline's fill (the
+    first upload) and drain (the last 2.4 ms download) are paid once per
+    stream, as a video would pay them; with 12 batches they were 10 % of
+    the time (rocprofv3 trace of scripts/e2e_probe.py: 4.6 ms per solve with
+    the downloads running beside it against 4.3 ms alone)."""
     import numpy as np
     import torch
     import hsflow
@@ -751,7 +756,8 @@ def e2e_leg(wl_name, args, dev, n_batches=12):
         bool(torch.equal(h_out[last][0], d_out[last][0].cpu())) and \
         bool(torch.equal(h_out[last][1], d_out[last][1].cpu()))
     return {"pairs_per_s_e2e": round(n_batches * batch / dt, 2),
-            "e2e": {"workload": f"{wl_name}, {batch} pairs per batch, {n_batches} batches",
+            "e2e": {"workload": f"{wl_name}, {batch} pairs per batch, {n_batches} batches "
+                                f"({n_batches * batch} pairs)",
                     "input": "pinned host u8 gray frames", "output": "pinned host f32 u, v",
                     "ms_per_batch": round(dt / n_batches * 1e3, 3),
                     "solve": "hipGraph replay" if graphs[0] is not None else "eager",
