@@ -655,11 +655,12 @@ def config1_leg(dev, reps=20):
 
 
 # --------------------------------------------------------------- e2e
-def e2e_leg(wl_name, args, dev, n_batches=48):
+def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
     """End-to-end pairs/s as BASELINE.md defines it: pinned host u8 gray
     frames (what main.cpp:13-14 hands over) -> H2D -> K1 + K2 -> D2H of u, v
     (f32), batch after batch.  Copies run on their own streams and overlap
-    the neighbouring batches' solves (double-buffered device slots).  The
+    the neighbouring batches' solves (`slots` device buffers in rotation: a
+    batch's upload, solve and download each have a slot of their own).  The
     downloads go through hsflow_download_device (the runtime's DMA engines):
     torch's copy_ into pinned memory runs as a 256-workgroup blit kernel per
     plane that takes the next batch's Jacobi workgroup slots (1275 vs ~1600
@@ -683,14 +684,14 @@ def e2e_leg(wl_name, args, dev, n_batches=48):
                         torch.from_numpy(np.stack([p[1] for p in ps])).pin_memory()))
     shp = (batch, rows, cols)
     d_in = [(torch.empty(shp, dtype=torch.uint8, device=dev),
-             torch.empty(shp, dtype=torch.uint8, device=dev)) for _ in range(2)]
+             torch.empty(shp, dtype=torch.uint8, device=dev)) for _ in range(slots)]
     d_out = [(torch.empty(shp, dtype=torch.float32, device=dev),
-              torch.empty(shp, dtype=torch.float32, device=dev)) for _ in range(2)]
+              torch.empty(shp, dtype=torch.float32, device=dev)) for _ in range(slots)]
     h_out = [(torch.empty(shp, dtype=torch.float32).pin_memory(),
-              torch.empty(shp, dtype=torch.float32).pin_memory()) for _ in range(2)]
-    ws = [hsflow.alloc_workspace(rows, cols, batch, dev) for _ in range(2)]
+              torch.empty(shp, dtype=torch.float32).pin_memory()) for _ in range(slots)]
+    ws = [hsflow.alloc_workspace(rows, cols, batch, dev) for _ in range(slots)]
     s_h2d, s_cmp, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
-    ev = {k: [torch.cuda.Event() for _ in range(2)]
+    ev = {k: [torch.cuda.Event() for _ in range(slots)]
           for k in ("in", "done", "in_free", "out_free")}
 
     def solve(sl, s):
@@ -699,11 +700,11 @@ def e2e_leg(wl_name, args, dev, n_batches=48):
 
     # each slot's solve is one hipGraph, as in the resident leg: eager, the
     # ~100 dependent launches of a solve leave dispatch gaps on the GPU
-    graphs = [None, None]
+    graphs = [None] * slots
     if not args.no_graph:
         try:
             cur = torch.cuda.current_stream(dev)
-            for sl in range(2):
+            for sl in range(slots):
                 cap = torch.cuda.Stream(dev)
                 cap.wait_stream(cur)
                 with torch.cuda.stream(cap):
@@ -717,21 +718,21 @@ def e2e_leg(wl_name, args, dev, n_batches=48):
             torch.cuda.synchronize(dev)
         except Exception as e:  # pragma: no cover - eager fallback, reported
             print(f"bench: e2e graph capture failed ({e}); eager solves", file=sys.stderr)
-            graphs = [None, None]
+            graphs = [None] * slots
 
     def run(n):
         for k in range(n):
-            sl = k % 2
+            sl = k % slots
             a, b = host_in[k % 2]
             with torch.cuda.stream(s_h2d):
-                if k >= 2:
+                if k >= slots:
                     s_h2d.wait_event(ev["in_free"][sl])
                 d_in[sl][0].copy_(a, non_blocking=True)
                 d_in[sl][1].copy_(b, non_blocking=True)
                 ev["in"][sl].record(s_h2d)
             with torch.cuda.stream(s_cmp):
                 s_cmp.wait_event(ev["in"][sl])
-                if k >= 2:
+                if k >= slots:
                     s_cmp.wait_event(ev["out_free"][sl])
                 if graphs[sl] is not None:
                     graphs[sl].replay()  # on s_cmp, the current stream
@@ -746,12 +747,12 @@ def e2e_leg(wl_name, args, dev, n_batches=48):
                 ev["out_free"][sl].record(s_d2h)
         torch.cuda.synchronize(dev)
 
-    run(2)  # warm-up (side streams, allocator)
+    run(slots)  # warm-up (side streams, allocator)
     t = time.perf_counter()
     run(n_batches)
     dt = time.perf_counter() - t
     # the last batch's flow arrived intact on the host
-    last = (n_batches - 1) % 2
+    last = (n_batches - 1) % slots
     ok = bool(torch.isfinite(h_out[last][0]).all()) and \
         bool(torch.equal(h_out[last][0], d_out[last][0].cpu())) and \
         bool(torch.equal(h_out[last][1], d_out[last][1].cpu()))
@@ -759,7 +760,7 @@ def e2e_leg(wl_name, args, dev, n_batches=48):
             "e2e": {"workload": f"{wl_name}, {batch} pairs per batch, {n_batches} batches "
                                 f"({n_batches * batch} pairs)",
                     "input": "pinned host u8 gray frames", "output": "pinned host f32 u, v",
-                    "ms_per_batch": round(dt / n_batches * 1e3, 3),
+                    "ms_per_batch": round(dt / n_batches * 1e3, 3), "slots": slots,
                     "solve": "hipGraph replay" if graphs[0] is not None else "eager",
                     "finite": ok}}
 
