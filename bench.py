@@ -747,7 +747,12 @@ def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
                 ev["out_free"][sl].record(s_d2h)
         torch.cuda.synchronize(dev)
 
-    run(slots)  # warm-up (side streams, allocator)
+    # warm-up, untimed: side streams, allocator, and the first DMA traffic
+    # into freshly pinned buffers -- the first pipelined run of a process
+    # read 4.7 ms per batch, later ones 4.16 (scripts/e2e_slots_ab.py,
+    # profiles/r04_e2e_slots_ab.jsonl); 12 batches absorb it, like the
+    # resident legs' pre-warm
+    run(max(slots, 12))
     t = time.perf_counter()
     run(n_batches)
     dt = time.perf_counter() - t
