@@ -655,6 +655,9 @@ def config1_leg(dev, reps=20):
 
 
 # --------------------------------------------------------------- e2e
+E2E_WARM_S = 0.4
+
+
 def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
     """End-to-end pairs/s as BASELINE.md defines it: pinned host u8 gray
     frames (what main.cpp:13-14 hands over) -> H2D -> K1 + K2 -> D2H of u, v
@@ -747,12 +750,16 @@ def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
                 ev["out_free"][sl].record(s_d2h)
         torch.cuda.synchronize(dev)
 
-    # warm-up, untimed: side streams, allocator, and the first DMA traffic
-    # into freshly pinned buffers -- the first pipelined run of a process
-    # read 4.7 ms per batch, later ones 4.16 (scripts/e2e_slots_ab.py,
-    # profiles/r04_e2e_slots_ab.jsonl); 12 batches absorb it, like the
-    # resident legs' pre-warm
-    run(max(slots, 12))
+    # warm-up, untimed, by time like the resident legs' pre-warm: the first
+    # pipelined run of a process read 4.6-4.7 ms per batch and every later
+    # one 4.15 (scripts/e2e_slots_ab.py, profiles/r04_e2e_slots_ab.jsonl),
+    # also after 12 untimed batches; copies and solves together need
+    # longer than the solves alone to reach their steady rate
+    t_end = time.perf_counter() + E2E_WARM_S
+    while True:
+        run(slots)
+        if time.perf_counter() >= t_end:
+            break
     t = time.perf_counter()
     run(n_batches)
     dt = time.perf_counter() - t
