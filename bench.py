@@ -817,13 +817,15 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
         stream = [tuple(torch.from_numpy(a).to(dev) for a in
                         hsflow.synth_pair(1000 + j, rows, cols)) for j in range(n)]
     mine = fp.my_pairs(n, rank, world)
-    # N > 1: each rank's share in groups of at most 8 pairs (at least 2), so
+    # each rank's share in groups of at most 8 pairs: 8 pairs fill the chip,
+    # and a group's planes (~330 MB per pass) partly stay in the 256 MB
+    # Infinity Cache between passes, which 64 pairs in one call (2.6 GB per
+    # pass) do not: one rank solved 64 pairs at 1.27 M Mpix*iter/s in one
+    # call against 1.35 M for 8-pair batches.  N > 1: at least 2 groups, so
     # group c+1 travels while group c is solved and group c's (u, v) travel
     # back while group c+1 is solved (frame_parallel.run_stream_pipelined;
-    # 8 pairs fill the chip, smaller groups start sooner:
-    # scripts/scale_predict.py); one rank has nothing to overlap and solves
-    # its share in one call
-    chunks = max(2, -(-len(mine) // 8)) if world > 1 else 1
+    # scripts/scale_predict.py)
+    chunks = max(2 if world > 1 else 1, -(-len(mine) // 8))
     if solve_batch is None:
         ws = hsflow.alloc_workspace(rows, cols, max(1, -(-len(mine) // chunks)), dev)
 
