@@ -59,7 +59,10 @@ def main():
              "1080p2": (2, 1080, 1920, 300), "8k1": (1, 4320, 7680, 60),
              "1080p32": (32, 1080, 1920, 60), "1080p64": (64, 1080, 1920, 120),
              "1080p32l": (32, 1080, 1920, 120), "1080p16": (16, 1080, 1920, 120),
-             "4k8": (8, 2160, 3840, 120), "4k4": (4, 2160, 3840, 120)}
+             "4k8": (8, 2160, 3840, 120), "4k4": (4, 2160, 3840, 120),
+             "1080p6": (6, 1080, 1920, 300), "1080p7": (7, 1080, 1920, 300),
+             "1080p8f": (8, 1080, 1920, 300), "1080p10": (10, 1080, 1920, 300),
+             "1080p12": (12, 1080, 1920, 300), "1080p16f": (16, 1080, 1920, 300)}
     hsflow.set_max_streams(a.streams)
     hsflow.set_iters_per_launch(a.kb)
     for name in a.cases.split(","):
