@@ -838,9 +838,20 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
         out[0] = fp.run_stream_pipelined(stream, n, (rows, cols), torch.float32, solve_batch,
                                          dev, rank, world, chunks=chunks)
 
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    warm = None
+    if dev.type == "cuda":
+        # untimed, rank-local clock warm-up: the rank's solve of one group of
+        # its own size, no collective inside, so ranks may run different
+        # counts (prewarm's rule); the timed passes are unchanged
+        g = max(1, -(-len(mine) // chunks))
+        gen = torch.Generator(device=dev).manual_seed(rank)
+        W0, W1 = (torch.rand((g, rows, cols), generator=gen, device=dev) * 255 for _ in "01")
+        n_w, t_w = prewarm(lambda: solve_batch(W0, W1), sync)
+        warm = {"prewarm_steps": n_w, "prewarm_s": round(t_w, 3), "pairs": g}
+        del W0, W1
     if world > 1:
         dist.barrier()  # every rank's communicator is up before the first P2P call
-    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     steps = max(1, min(args.steps, 3))
     elapsed = timed_region(one_pass, sync, steps, 1, world, dev)
     leg = {"pairs_per_s": round(n * steps / elapsed, 2),
@@ -849,6 +860,8 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
            "Mpix_iter_per_s": round(n * steps * rows * cols * iters / elapsed / 1e6, 1),
            "transport": _transport(world, dev),
            "scaling": "strong"}
+    if warm is not None:
+        leg["untimed_prewarm"] = warm
     if rank == 0:
         res = out[0]
         leg["gathered"] = len(res) if res is not None else 0
