@@ -814,8 +814,17 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
     n = n_pairs or args.pairs
     stream = None
     if rank == 0:
-        stream = [tuple(torch.from_numpy(a).to(dev) for a in
-                        hsflow.synth_pair(1000 + j, rows, cols)) for j in range(n)]
+        # the stream's frames back to back in one device buffer per frame
+        # slot (as a decoder writing into one allocation leaves them): a
+        # group of consecutive pairs is then a view, not a stacked copy
+        # (frame_parallel.batch_of)
+        A = torch.empty((n, rows, cols), dtype=torch.float32, device=dev)
+        B = torch.empty_like(A)
+        for j in range(n):
+            a, b = hsflow.synth_pair(1000 + j, rows, cols)
+            A[j].copy_(torch.from_numpy(a))
+            B[j].copy_(torch.from_numpy(b))
+        stream = [(A[j], B[j]) for j in range(n)]
     mine = fp.my_pairs(n, rank, world)
     # each rank's share in groups of at most 8 pairs: 8 pairs fill the chip,
     # and a group's planes (~330 MB per pass) partly stay in the 256 MB

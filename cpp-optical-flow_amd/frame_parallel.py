@@ -118,6 +118,22 @@ def chunk_split(mine: Sequence[int], chunks: int) -> List[List[int]]:
     return out
 
 
+def batch_of(frames: Sequence[torch.Tensor], device) -> torch.Tensor:
+    """The frames as one (len, rows, cols) batch: a view when they already
+    lie back to back in one device buffer (a stream decoded into one
+    allocation, as bench.py holds it), else a stacked copy."""
+    f0 = frames[0]
+    if f0.device == torch.device(device) and all(f.is_contiguous() for f in frames):
+        step = f0.numel() * f0.element_size()
+        base = f0.untyped_storage().data_ptr()
+        if all(f.untyped_storage().data_ptr() == base and
+               f.data_ptr() == f0.data_ptr() + k * step and f.shape == f0.shape
+               and f.dtype == f0.dtype for k, f in enumerate(frames)):
+            return f0.as_strided((len(frames),) + tuple(f0.shape),
+                                 (f0.numel(),) + tuple(f0.stride()))
+    return torch.stack([f.to(device) for f in frames])
+
+
 def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, dtype,
                          solve_batch: Callable[[torch.Tensor, torch.Tensor], Pair], device,
                          rank: int, world: int, chunks: int = 2, gather: bool = True):
@@ -142,8 +158,8 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
     if world == 1:
         out: List[Pair] = []
         for grp in chunk_split(mine, chunks):
-            I0 = torch.stack([stream[j][0].to(device) for j in grp])
-            I1 = torch.stack([stream[j][1].to(device) for j in grp])
+            I0 = batch_of([stream[j][0] for j in grp], device)
+            I1 = batch_of([stream[j][1] for j in grp], device)
             u, v = solve_batch(I0, I1)
             out.extend((u[k], v[k]) for k in range(len(grp)))
         return out if gather else None
@@ -201,8 +217,8 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
         if c < len(groups[rank]):
             grp = groups[rank][c]
             if rank == 0:
-                I0 = torch.stack([stream[j][0].to(device) for j in grp])
-                I1 = torch.stack([stream[j][1].to(device) for j in grp])
+                I0 = batch_of([stream[j][0] for j in grp], device)
+                I1 = batch_of([stream[j][1] for j in grp], device)
             else:
                 I0, I1, reqs = recv_groups[c]
                 for req in reqs:

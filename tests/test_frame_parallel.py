@@ -159,6 +159,29 @@ def test_pipelined_single_rank_groups():
         assert np.array_equal(out[j][0].numpy(), u.numpy())
 
 
+def test_batch_of_views_back_to_back_frames():
+    """Frames that lie back to back in one buffer batch as a view (no copy);
+    anything else is stacked; both equal torch.stack."""
+    A = torch.arange(5 * 4 * 6, dtype=torch.float32).reshape(5, 4, 6)
+    cpu = torch.device("cpu")
+    b = fp.batch_of([A[1], A[2], A[3]], cpu)
+    assert b.data_ptr() == A[1].data_ptr() and torch.equal(b, A[1:4])
+    for frames in ([A[0], A[2]], [A[3], A[2]], [A[1], A[1].clone()], [A[0, :, :3], A[1, :, :3]]):
+        b = fp.batch_of(frames, cpu)
+        assert b.untyped_storage().data_ptr() != A.untyped_storage().data_ptr()  # a copy
+        assert torch.equal(b, torch.stack(frames))
+    # the single-rank pipeline over a back-to-back stream gives the same flows
+    S = _stream()
+    A0 = torch.stack([p[0] for p in S])
+    A1 = torch.stack([p[1] for p in S])
+    out = fp.run_stream_pipelined([(A0[j], A1[j]) for j in range(N_PAIRS)], N_PAIRS,
+                                  (ROWS, COLS), torch.float32, _solve_batch, cpu, 0, 1,
+                                  chunks=2)
+    for j, (I0, I1) in enumerate(S):
+        u, v = _solve(I0, I1)
+        assert np.array_equal(out[j][0].numpy(), u.numpy())
+
+
 # ---- the same protocol with the real HIP solver (2 processes, one GPU) ----
 
 def _gpu_solve(I0, I1):
