@@ -45,3 +45,59 @@ def test_download_device_rejects_mismatched_sizes(hs):
     import torch
     with pytest.raises(hs.HsflowError):
         hs.download_device(torch.empty(8).pin_memory(), torch.empty(9, device="cuda"))
+
+
+@pytest.mark.gpu
+def test_host_call_context_reuse_is_bit_exact(hs):
+    """One context through a frame loop (main.cpp:97-98): repeated calls
+    reuse its grow-only device buffers and must give a fresh context's bits
+    across new frames, new parameters (alpha, iterations, window), a larger
+    frame and back, f32 frames and a launch override."""
+    import numpy as np
+    a, b = hs.synth_pair(7, 270, 480)
+    a8, b8 = a.astype(np.uint8), b.astype(np.uint8)
+    c, d = hs.synth_pair(8, 270, 480)
+    c8, d8 = c.astype(np.uint8), d.astype(np.uint8)
+    big0, big1 = (x.astype(np.uint8) for x in hs.synth_pair(9, 540, 960))
+
+    def fresh(I0, I1, w, n, alpha):
+        with hs.Context(0) as ctx:  # one call per context: always eager
+            return ctx.flow(I0, I1, w, n, alpha)
+
+    ref = fresh(a8, b8, 5, 40, 1.0)
+    with hs.Context(0) as ctx:
+        for _ in range(4):
+            u, v = ctx.flow(a8, b8, 5, 40, 1.0)
+            assert np.array_equal(u, ref[0]) and np.array_equal(v, ref[1])
+        # new frames, same buffers and parameters
+        ref_cd = fresh(c8, d8, 5, 40, 1.0)
+        for _ in range(3):
+            u, v = ctx.flow(c8, d8, 5, 40, 1.0)
+            assert np.array_equal(u, ref_cd[0]) and np.array_equal(v, ref_cd[1])
+        # parameters change: alpha, iterations, window
+        for args in ((5, 40, 3.0), (5, 41, 3.0), (3, 41, 3.0)):
+            want = fresh(a8, b8, *args)
+            for _ in range(3):
+                u, v = ctx.flow(a8, b8, *args)
+                assert np.array_equal(u, want[0]) and np.array_equal(v, want[1]), args
+        # a larger frame grows the device buffers, then back to the small one
+        want_big = fresh(big0, big1, 5, 40, 1.0)
+        for _ in range(3):
+            u, v = ctx.flow(big0, big1, 5, 40, 1.0)
+            assert np.array_equal(u, want_big[0]) and np.array_equal(v, want_big[1])
+        for _ in range(3):
+            u, v = ctx.flow(a8, b8, 5, 40, 1.0)
+            assert np.array_equal(u, ref[0]) and np.array_equal(v, ref[1])
+        # f32 frames take the f32-gradient variant as well
+        want_f = fresh(a, b, 5, 40, 1.0)
+        for _ in range(3):
+            u, v = ctx.flow(a, b, 5, 40, 1.0)
+            assert np.array_equal(u, want_f[0]) and np.array_equal(v, want_f[1])
+        # a launch override between two identical calls is part of the key
+        try:
+            hs.set_jacobi_kernel(2)
+            for _ in range(3):
+                u, v = ctx.flow(a8, b8, 5, 40, 1.0)
+                assert np.array_equal(u, ref[0]) and np.array_equal(v, ref[1])
+        finally:
+            hs.set_jacobi_kernel(0)
