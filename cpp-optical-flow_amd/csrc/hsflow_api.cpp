@@ -420,8 +420,9 @@ int gradients_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in
     if (ws_bytes < w.bytes)
         return fail(ctx, HSFLOW_ERR_ARG, "workspace %zu < %zu bytes", ws_bytes, w.bytes);
     HIP_TRY(ctx, hipMemsetAsync(w.flags, 0, (size_t)batch * 4, s));
+    // the f32 planes for every pair only when the caller takes them
     hipError_t e = hsflow::launch_gradients(I0, I1, dtype_in, rows, cols, batch, w.gpack,
-                                            w.gx, w.gy, w.gt, w.flags, s);
+                                            w.gx, w.gy, w.gt, w.flags, gx || gy || gt, s);
     if (e != hipSuccess) return hip_fail(ctx, e, "gradients launch");
     const size_t n = (size_t)rows * cols * batch;
     if (gx) HIP_TRY(ctx, hipMemcpyAsync(gx, w.gx, n * 4, hipMemcpyDeviceToDevice, s));

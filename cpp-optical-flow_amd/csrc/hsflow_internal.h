@@ -25,9 +25,11 @@ struct JacobiArgs {
                                // that do not fill the chip (fill_limited)
 };
 
+// K1 (+ K1f): packed gradients and flags; the f32 planes for every pair
+// when `planes` (the gradients API), else only for the flagged pairs
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
                             int cols, int batch, uint32_t *gpack, float *gx, float *gy,
-                            float *gt, uint32_t *flags, hipStream_t s);
+                            float *gt, uint32_t *flags, bool planes, hipStream_t s);
 hipError_t launch_jacobi(JacobiArgs a, int W, int KB, hipStream_t s);
 // config 5 pyramid (hsflow_pyramid.hip); dtype as HSFLOW_U8/F32/F16
 hipError_t launch_pyrdown(const void *src, int dtype, int rows, int cols, int batch,

@@ -30,6 +30,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "hsflow_internal.h"
 #include "hsflow_device.h"
@@ -52,8 +53,33 @@ template <typename T> struct GradMath { using type = float; };
 template <> struct GradMath<double> { using type = double; };
 
 // ----------------------------------------------------------------------- K1
+// Sobel dx, dy (ksize 3, reflect-101) and dt at pixel (r, c) of one pair,
+// hornSchunck.cpp:27-28 and :39; exact for 8-bit-valued data.  Shared by K1
+// and K1f so the f32 planes hold the same values whichever kernel writes them.
+template <typename T, typename F>
+__device__ __forceinline__ void sobel_at(const T *a, const T *b, int rows, int cols, int r,
+                                         int c, F &dx, F &dy, F &dt, F &z_0, F &nxt) {
+    const int rm = reflect101(r - 1, rows), rp = reflect101(r + 1, rows);
+    const int cm = reflect101(c - 1, cols), cp = reflect101(c + 1, cols);
+    const T *pm = a + (size_t)rm * cols, *p0 = a + (size_t)r * cols,
+            *pp = a + (size_t)rp * cols;
+    const F m_m = (F)pm[cm], m_0 = (F)pm[c], m_p = (F)pm[cp];
+    const F z_m = (F)p0[cm], z_p = (F)p0[cp];
+    const F p_m = (F)pp[cm], p_0 = (F)pp[c], p_p = (F)pp[cp];
+    z_0 = (F)p0[c];
+    nxt = (F)b[(size_t)r * cols + c];
+    dx = (m_p - m_m) + (F)2 * (z_p - z_m) + (p_p - p_m);
+    dy = (p_m - m_m) + (F)2 * (p_0 - m_0) + (p_p - m_p);
+    dt = nxt - z_0;
+}
+
+// K1: packed exact gradients and the per-pair integrality flag; with PLANES
+// also the f32 gradient planes (the gradients API hands them out).  Without
+// PLANES the planes are written by K1f for the flagged pairs only -- the
+// only pairs whose Jacobi passes read them -- which takes 12 of K1's 24 B
+// per pixel of f32 frames off every solve.
 // block 64 x 4, one pixel per thread; grid (ceil(cols/64), ceil(rows/4), batch)
-template <typename T>
+template <typename T, bool PLANES>
 __global__ __launch_bounds__(256) void hs_gradients_kernel(
     const T *__restrict__ I0, const T *__restrict__ I1, int rows, int cols,
     uint32_t *__restrict__ gpack, float *__restrict__ gx, float *__restrict__ gy,
@@ -62,32 +88,48 @@ __global__ __launch_bounds__(256) void hs_gradients_kernel(
     const int c = blockIdx.x * 64 + threadIdx.x;
     const int r = blockIdx.y * 4 + threadIdx.y;
     const size_t plane = (size_t)rows * cols;
-    const T *a = I0 + blockIdx.z * plane;
-    const T *b = I1 + blockIdx.z * plane;
     bool bad = false;
     if (r < rows && c < cols) {
-        const int rm = reflect101(r - 1, rows), rp = reflect101(r + 1, rows);
-        const int cm = reflect101(c - 1, cols), cp = reflect101(c + 1, cols);
-        const T *pm = a + (size_t)rm * cols, *p0 = a + (size_t)r * cols,
-                *pp = a + (size_t)rp * cols;
-        const F m_m = (F)pm[cm], m_0 = (F)pm[c], m_p = (F)pm[cp];
-        const F z_m = (F)p0[cm], z_0 = (F)p0[c], z_p = (F)p0[cp];
-        const F p_m = (F)pp[cm], p_0 = (F)pp[c], p_p = (F)pp[cp];
-        const F nxt = (F)b[(size_t)r * cols + c];
-        // hornSchunck.cpp:27-28 (Sobel ksize 3) and :39; exact for 8-bit data
-        const F dx = (m_p - m_m) + (F)2 * (z_p - z_m) + (p_p - p_m);
-        const F dy = (p_m - m_m) + (F)2 * (p_0 - m_0) + (p_p - m_p);
-        const F dt = nxt - z_0;
+        F dx, dy, dt, z_0, nxt;
+        sobel_at(I0 + blockIdx.z * plane, I1 + blockIdx.z * plane, rows, cols, r, c, dx, dy,
+                 dt, z_0, nxt);
         const size_t o = blockIdx.z * plane + (size_t)r * cols + c;
-        gx[o] = (float)dx;
-        gy[o] = (float)dy;
-        gt[o] = (float)dt;
+        if constexpr (PLANES) {
+            gx[o] = (float)dx;
+            gy[o] = (float)dy;
+            gt[o] = (float)dt;
+        }
         // packed form is exact iff both frames are integers in [0, 255]
         bad = !(z_0 == rint(z_0) && nxt == rint(nxt) && z_0 >= (F)0 && z_0 <= (F)255 &&
                 nxt >= (F)0 && nxt <= (F)255);
         gpack[o] = pack_grad((int)dx, (int)dy, (int)dt);
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[blockIdx.z], 1u);
+}
+
+// K1f: the f32 gradient planes of the pairs K1 flagged as non-integral;
+// the other pairs' workgroups return at once.  Grid (kK1fBlocks, batch),
+// 256 threads, grid-stride over the pair's pixels.
+constexpr int kK1fBlocks = 256;
+template <typename T>
+__global__ __launch_bounds__(256) void hs_gradients_f32_kernel(
+    const T *__restrict__ I0, const T *__restrict__ I1, int rows, int cols,
+    float *__restrict__ gx, float *__restrict__ gy, float *__restrict__ gt,
+    const uint32_t *__restrict__ flags) {
+    using F = typename GradMath<T>::type;
+    if (flags[blockIdx.y] == 0u) return;  // whole workgroup: uniform
+    const size_t plane = (size_t)rows * cols;
+    const T *a = I0 + blockIdx.y * plane, *b = I1 + blockIdx.y * plane;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < plane;
+         i += (size_t)gridDim.x * 256) {
+        const int r = (int)(i / (size_t)cols), c = (int)(i - (size_t)r * cols);
+        F dx, dy, dt, z_0, nxt;
+        sobel_at(a, b, rows, cols, r, c, dx, dy, dt, z_0, nxt);
+        const size_t o = blockIdx.y * plane + i;
+        gx[o] = (float)dx;
+        gy[o] = (float)dy;
+        gt[o] = (float)dt;
+    }
 }
 
 // ----------------------------------------------------------------------- K2
@@ -933,26 +975,40 @@ __global__ __launch_bounds__(256) void hs_jacobi_generic_kernel(const JacobiArgs
 }
 
 // ------------------------------------------------------------------ launchers
+template <typename T>
+static void launch_gradients_t(const void *I0, const void *I1, int rows, int cols, int batch,
+                               uint32_t *gpack, float *gx, float *gy, float *gt,
+                               uint32_t *flags, bool planes, hipStream_t s) {
+    dim3 blk(64, 4, 1), grd((cols + 63) / 64, (rows + 3) / 4, batch);
+    const T *a = (const T *)I0, *b = (const T *)I1;
+    if (planes) {
+        hipLaunchKernelGGL((hs_gradients_kernel<T, true>), grd, blk, 0, s, a, b, rows, cols,
+                           gpack, gx, gy, gt, flags);
+        return;
+    }
+    hipLaunchKernelGGL((hs_gradients_kernel<T, false>), grd, blk, 0, s, a, b, rows, cols, gpack,
+                       gx, gy, gt, flags);
+    // 8-bit frames are always integral: no pair is ever flagged
+    if constexpr (!std::is_same<T, uint8_t>::value)
+        hipLaunchKernelGGL(hs_gradients_f32_kernel<T>, dim3(kK1fBlocks, batch), dim3(256), 0, s,
+                           a, b, rows, cols, gx, gy, gt, flags);
+}
+
 hipError_t launch_gradients(const void *I0, const void *I1, int dtype_in, int rows,
                             int cols, int batch, uint32_t *gpack, float *gx, float *gy,
-                            float *gt, uint32_t *flags, hipStream_t s) {
-    dim3 blk(64, 4, 1), grd((cols + 63) / 64, (rows + 3) / 4, batch);
+                            float *gt, uint32_t *flags, bool planes, hipStream_t s) {
     if (dtype_in == 0)
-        hipLaunchKernelGGL(hs_gradients_kernel<uint8_t>, grd, blk, 0, s,
-                           (const uint8_t *)I0, (const uint8_t *)I1, rows, cols, gpack,
-                           gx, gy, gt, flags);
+        launch_gradients_t<uint8_t>(I0, I1, rows, cols, batch, gpack, gx, gy, gt, flags, planes,
+                                    s);
     else if (dtype_in == 2)  // HSFLOW_F64 (CV_64FC1 frames)
-        hipLaunchKernelGGL(hs_gradients_kernel<double>, grd, blk, 0, s,
-                           (const double *)I0, (const double *)I1, rows, cols, gpack,
-                           gx, gy, gt, flags);
+        launch_gradients_t<double>(I0, I1, rows, cols, batch, gpack, gx, gy, gt, flags, planes,
+                                   s);
     else if (dtype_in == 3)  // HSFLOW_F16 (config 5 inputs)
-        hipLaunchKernelGGL(hs_gradients_kernel<_Float16>, grd, blk, 0, s,
-                           (const _Float16 *)I0, (const _Float16 *)I1, rows, cols, gpack,
-                           gx, gy, gt, flags);
+        launch_gradients_t<_Float16>(I0, I1, rows, cols, batch, gpack, gx, gy, gt, flags,
+                                     planes, s);
     else
-        hipLaunchKernelGGL(hs_gradients_kernel<float>, grd, blk, 0, s,
-                           (const float *)I0, (const float *)I1, rows, cols, gpack, gx,
-                           gy, gt, flags);
+        launch_gradients_t<float>(I0, I1, rows, cols, batch, gpack, gx, gy, gt, flags, planes,
+                                  s);
     return hipGetLastError();
 }
 
