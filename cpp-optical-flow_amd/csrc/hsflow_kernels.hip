@@ -11,6 +11,8 @@
 //      complement), so a Jacobi pass streams 4 B of gradients per pixel
 //      instead of 12.  Non-integral inputs set a per-pair flag; the Jacobi
 //      kernels then read that pair's f32 gradient planes.
+//  K1f hs_gradients_f32_kernel  those f32 planes, for the flagged pairs only
+//      (K1 writes them for every pair only when the gradients API takes them).
 //
 //  K2  hs_jacobi_wg_kernel   hornSchunck.cpp:56-74, windows 3..9: one pass
 //      of KB Jacobi iterations on register-resident 128-column tiles (eight
