@@ -419,7 +419,8 @@ int gradients_impl(hsflow_ctx *ctx, const void *I0, const void *I1, int dtype_in
     Workspace w = carve(workspace, rows, cols, batch);
     if (ws_bytes < w.bytes)
         return fail(ctx, HSFLOW_ERR_ARG, "workspace %zu < %zu bytes", ws_bytes, w.bytes);
-    HIP_TRY(ctx, hipMemsetAsync(w.flags, 0, (size_t)batch * 4, s));
+    // K1 stores 8-bit frames' flags itself (always 0); the others OR into zeros
+    if (dtype_in != HSFLOW_U8) HIP_TRY(ctx, hipMemsetAsync(w.flags, 0, (size_t)batch * 4, s));
     // the f32 planes for every pair only when the caller takes them
     hipError_t e = hsflow::launch_gradients(I0, I1, dtype_in, rows, cols, batch, w.gpack,
                                             w.gx, w.gy, w.gt, w.flags, gx || gy || gt, s);

@@ -106,7 +106,14 @@ __global__ __launch_bounds__(256) void hs_gradients_kernel(
                 nxt >= (F)0 && nxt <= (F)255);
         gpack[o] = pack_grad((int)dx, (int)dy, (int)dt);
     }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[blockIdx.z], 1u);
+    if constexpr (std::is_same<T, uint8_t>::value) {
+        // 8-bit frames are always integral: the flag is a plain 0, stored
+        // by one thread of the pair (no zeroing memset before K1)
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0)
+            flags[blockIdx.z] = 0u;
+    } else if (__any(bad) && (threadIdx.x & 63) == 0) {
+        atomicOr(&flags[blockIdx.z], 1u);
+    }
 }
 
 // K1f: the f32 gradient planes of the pairs K1 flagged as non-integral;
