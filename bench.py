@@ -391,8 +391,7 @@ def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
     launches_per_solve = -(-iters // kb)
     # one stream so the per-launch duration is what rocprofv3 reports per
     # dispatch (the batch split overlaps launches and would blur it)
-    hsflow.set_max_streams(1)
-    try:
+    with hsflow.max_streams_as(1):
         hsflow.jacobi_device(rows, cols, batch, window, iters, alpha, u, v, rws, stream=stream)
         torch.cuda.synchronize(dev)
         ev0.record(stream)
@@ -401,8 +400,6 @@ def roofline_leg(wl_name, hsflow, dev, I0, I1, rows, cols, batch, window, iters,
                                  stream=stream)
         ev1.record(stream)
         torch.cuda.synchronize(dev)
-    finally:
-        hsflow.set_max_streams(0)
     k2_ms = ev0.elapsed_time(ev1) / (reps * launches_per_solve)
     n_px = batch * rows * cols
     # algorithmic bytes of one blocked pass: u, v in (the first pass of a
@@ -528,7 +525,10 @@ def resident_leg(wl_name, args, dev, world, rank, init_dist=None, window=None, b
             # thread_local: only this thread's calls can invalidate the
             # capture (the secondary leg captures after the process group,
             # whose watchdog thread polls events, is up)
-            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            # the capture's origin stream calls the library itself, so the
+            # batch split (automatic: off under capture) is safe to ask for
+            with hsflow.max_streams_as(2), \
+                    torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 solve(torch.cuda.current_stream(dev))
             torch.cuda.synchronize(dev)
         except Exception as e:  # pragma: no cover - eager fallback, reported
@@ -715,7 +715,8 @@ def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
                 cur.wait_stream(cap)
                 torch.cuda.synchronize(dev)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with hsflow.max_streams_as(2), \
+                        torch.cuda.graph(g, capture_error_mode="thread_local"):
                     solve(sl, torch.cuda.current_stream(dev))
                 graphs[sl] = g
             torch.cuda.synchronize(dev)

@@ -51,6 +51,9 @@ int g_kb_override = 0;
 int g_kernel_override = 0;
 // K4 rows per segment (hsflow_set_strip_rows): 0 = automatic
 int g_strip_rows = 0;
+// K4 segment shape (hsflow_set_strip_segments): 0 = automatic (parallelogram
+// where the segment height allows it), 1 = rectangles, 2 = parallelograms
+int g_strip_segments = 0;
 
 // Kernel and blocking depth of a launch's passes.  K4 (streaming strips)
 // runs the full-depth passes when it is built for the window's default
@@ -119,6 +122,11 @@ struct Workspace {
     uint32_t *gpack;
     float *gx, *gy, *gt, *u2, *v2;
     uint32_t *flags;
+    // K4 parallelogram exchange: per pair hsflow::strip_pg_slots slots and
+    // as many flags (hsflow_strips.hip)
+    float *xch;
+    uint32_t *xflag;
+    size_t xslots;  // per pair
     size_t bytes;
 };
 
@@ -138,6 +146,9 @@ Workspace carve(void *base, int rows, int cols, int batch) {
     w.u2 = (float *)take(n * 4);
     w.v2 = (float *)take(n * 4);
     w.flags = (uint32_t *)take((size_t)batch * 4);
+    w.xslots = hsflow::strip_pg_slots(rows, cols);
+    w.xch = (float *)take(w.xslots * batch * hsflow::strip_pg_slot_bytes());
+    w.xflag = (uint32_t *)take(w.xslots * batch * 4);
     w.bytes = off;
     return w;
 }
@@ -211,9 +222,24 @@ struct SidePool {
     std::vector<hipEvent_t> events;  // [0] fork, [1..] joins
 };
 
+// hsflow_set_max_streams: 0 = automatic (split in 2 eagerly, not at all
+// while the caller's stream is capturing), n >= 1 = up to n streams always
 int g_split_override = 0;
 
-int max_split() { return g_split_override > 0 ? g_split_override : 2; }
+// Streams a batch of `batch` pairs on `s` is split over.  Under stream
+// capture the automatic choice does not split: a stream forked inside a
+// capture from a capturing stream that is not the capture's origin crashes
+// hipStreamEndCapture on ROCm 7.2 (profiles/r04_capture_crash.txt; legal in
+// CUDA), and the library cannot tell an origin from a forked stream.  A
+// caller that captures on the origin itself may ask for the split with
+// hsflow_set_max_streams(n >= 2) (the bench's timed graphs do).
+int split_for(int batch, hipStream_t s) {
+    if (g_split_override > 0) return std::min(batch, g_split_override);
+    if (batch < 2) return 1;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return 1;
+    return 2;
+}
 
 SidePool *side_pool(int need) {
     // one pool per device and thread: a thread that alternates devices keeps
@@ -253,7 +279,7 @@ int jacobi_impl(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int 
     int rc0 = check_jacobi_args(ctx, rows, cols, batch, window, iters, u, v, workspace,
                                 ws_bytes);
     if (rc0) return rc0;
-    const int split = std::min(batch, max_split());
+    const int split = split_for(batch, s);
     if (split <= 1 || iters == 0)
         return jacobi_one(ctx, rows, cols, batch, window, iters, alpha, warm, maybe_f32, u,
                           v, workspace, ws_bytes, s);
@@ -264,20 +290,29 @@ int jacobi_impl(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int 
                           v, workspace, ws_bytes, s);
     const size_t plane = (size_t)rows * cols;
     HIP_TRY(ctx, hipEventRecord(pool->events[0], s));
-    int first = 0;
-    for (int k = 0; k < split; ++k) {
+    int first = 0, forked = 0, rc = HSFLOW_OK;
+    for (int k = 0; k < split && rc == HSFLOW_OK; ++k) {
         const int nb = batch / split + (k < batch % split ? 1 : 0);
         hipStream_t sk = pool->streams[k];
-        HIP_TRY(ctx, hipStreamWaitEvent(sk, pool->events[0], 0));
+        hipError_t e = hipStreamWaitEvent(sk, pool->events[0], 0);
+        if (e != hipSuccess) {
+            rc = hip_fail(ctx, e, "hipStreamWaitEvent (fork)");
+            break;
+        }
+        ++forked;
         // the sub-batch's slice of every workspace plane, as its own workspace
-        int rc = jacobi_sub(ctx, rows, cols, nb, first, batch, window, iters, alpha, warm,
-                            maybe_f32, u + first * plane, v + first * plane, w, sk);
-        if (rc) return rc;
-        HIP_TRY(ctx, hipEventRecord(pool->events[1 + k], sk));
+        rc = jacobi_sub(ctx, rows, cols, nb, first, batch, window, iters, alpha, warm,
+                        maybe_f32, u + first * plane, v + first * plane, w, sk);
         first += nb;
     }
-    for (int k = 0; k < split; ++k) HIP_TRY(ctx, hipStreamWaitEvent(s, pool->events[1 + k], 0));
-    return HSFLOW_OK;
+    // join every forked stream back, the error path included (a capture
+    // must not be left with streams that never rejoin its origin)
+    for (int k = 0; k < forked; ++k) {
+        hipError_t e = hipEventRecord(pool->events[1 + k], pool->streams[k]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, pool->events[1 + k], 0);
+        if (e != hipSuccess && rc == HSFLOW_OK) rc = hip_fail(ctx, e, "stream join");
+    }
+    return rc;
 }
 
 // The Jacobi passes of `batch` pairs whose workspace planes are `w` (a view
@@ -321,6 +356,18 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
     a.flags = w.flags;
     a.write_through =
         hsflow::fill_limited(window, kb, strip, rows, cols, fill_batch, strip_rows) ? 1 : 0;
+    // K4 parallelogram segments where the height allows them (identical
+    // bits; the flags are zeroed once per solve, each launch leaves them 0)
+    const bool pg = strip && g_strip_segments == 2 && iters >= kb &&
+                    hsflow::strip_pg_ok(window, kb, strip_rows);
+    if (strip && g_strip_segments == 2 && !pg && iters >= kb)
+        return fail(ctx, HSFLOW_ERR_ARG, "K4 parallelogram segments need whole unroll periods "
+                    "of >= %d rows (segment height %d)", hsflow::kStripPgMinRows, strip_rows);
+    if (pg) {
+        a.xch = w.xch;
+        a.xflag = w.xflag;
+        HIP_TRY(ctx, hipMemsetAsync(w.xflag, 0, w.xslots * batch * 4, s));
+    }
     // pass p writes the caller's buffers iff (passes-1-p) is even, so the
     // last pass always lands in (u, v)
     auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };
@@ -403,6 +450,8 @@ int jacobi_sub(hsflow_ctx *ctx, int rows, int cols, int nb, int first, int batch
     sub.u2 = w.u2 + off;
     sub.v2 = w.v2 + off;
     sub.flags = w.flags + first;
+    sub.xch = (float *)((char *)w.xch + w.xslots * first * hsflow::strip_pg_slot_bytes());
+    sub.xflag = w.xflag + w.xslots * first;
     // the split's halves run concurrently: the depth is chosen for the batch
     return run_passes(ctx, rows, cols, nb, window, iters, alpha, warm, maybe_f32, u, v, sub,
                       s, batch);
@@ -708,6 +757,12 @@ int hsflow_set_jacobi_kernel(int k) {
     return HSFLOW_OK;
 }
 
+int hsflow_set_strip_segments(int mode) {
+    if (mode < 0 || mode > 2) return HSFLOW_ERR_ARG;
+    g_strip_segments = mode;
+    return HSFLOW_OK;
+}
+
 int hsflow_set_strip_rows(int seg_rows) {
     if (seg_rows < 0 || seg_rows > kMaxRows) return HSFLOW_ERR_ARG;
     g_strip_rows = seg_rows;
@@ -726,6 +781,8 @@ int hsflow_set_max_streams(int n) {
     g_split_override = n;
     return HSFLOW_OK;
 }
+
+int hsflow_max_streams(void) { return g_split_override; }
 
 int hsflow_iters_per_launch(int rows, int cols, int batch, int window) {
     if (window < 1 || window > HSFLOW_MAX_WINDOW) return HSFLOW_ERR_ARG;
@@ -849,9 +906,12 @@ int hsflow_flow_multi(const int *devices, int n_devices, int batch,
                                 window, iters, alpha, u[j], v[j], dtype_out, out_step);
             if (r) {
                 msg[k] = hsflow_last_error(ctx);
-                // a context that hit an error is not trusted with the next call
-                hsflow_destroy(ctx);
-                slot[k]->ctx = nullptr;
+                // a context that hit a runtime error is not trusted with the
+                // next call; argument and size errors leave it as it was
+                if (r != HSFLOW_ERR_ARG && r != HSFLOW_ERR_SIZE) {
+                    hsflow_destroy(ctx);
+                    slot[k]->ctx = nullptr;
+                }
             }
             rc[k] = r;
         });

@@ -52,6 +52,7 @@ EXPORTS = (
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
     "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
     "hsflow_download_device", "hsflow_jacobi_kernel_name", "hsflow_set_strip_rows",
+    "hsflow_set_strip_segments", "hsflow_max_streams",
     "hsflow_flow_multi_release",
 )
 BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
@@ -112,8 +113,10 @@ def lib():
     L.hsflow_set_iters_per_launch.argtypes = [i]
     L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
     L.hsflow_set_max_streams.argtypes = [i]
+    L.hsflow_max_streams.argtypes = []
     L.hsflow_set_jacobi_kernel.argtypes = [i]
     L.hsflow_set_strip_rows.argtypes = [i]
+    L.hsflow_set_strip_segments.argtypes = [i]
     L.hsflow_jacobi_kernel_name.argtypes = [i, i, i, i]
     L.hsflow_jacobi_kernel_name.restype = ctypes.c_char_p
     L.hsflow_pyramid_level_size.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
@@ -620,8 +623,30 @@ def set_iters_per_launch(k: int):
 
 
 def set_max_streams(n: int):
-    """Side streams a batch is split over (1 = off, 0 = default)."""
+    """Side streams a batch is split over: 0 = automatic (2 for eager calls,
+    none under stream capture), n >= 1 = up to n always."""
     _check(lib().hsflow_set_max_streams(int(n)))
+
+
+def max_streams() -> int:
+    """The current set_max_streams setting (0 = automatic)."""
+    return int(lib().hsflow_max_streams())
+
+
+class max_streams_as:
+    """Context manager: set_max_streams(n) inside, the previous setting after."""
+
+    def __init__(self, n: int):
+        self.n = int(n)
+
+    def __enter__(self):
+        self.prev = max_streams()
+        set_max_streams(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        set_max_streams(self.prev)
+        return False
 
 
 def set_jacobi_kernel(k: int):
@@ -634,6 +659,12 @@ def set_jacobi_kernel(k: int):
 def set_strip_rows(seg_rows: int = 0):
     """K4 rows per segment (0 = automatic); identical bits for any choice."""
     _check(lib().hsflow_set_strip_rows(int(seg_rows)))
+
+
+def set_strip_segments(mode: int = 0):
+    """K4 segment shape: 0 automatic (parallelograms where the height allows),
+    1 rectangles, 2 parallelograms.  Identical bits (A/B and tests only)."""
+    _check(lib().hsflow_set_strip_segments(int(mode)))
 
 
 def jacobi_kernel_name(rows, cols, batch, window) -> str:

@@ -665,6 +665,7 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
     rank_streams = any(getattr(o, "stream", None) is not None for o in ops_list)
     g = torch.cuda.CUDAGraph()
     import hsflow
+    prev_split = hsflow.max_streams()
     if rank_streams:
         # Inside a capture, a stream forked from a capturing stream that is
         # not the capture's origin -- here: a rank stream's side stream, or
@@ -673,7 +674,9 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
         # side2, also when the side stream joined the capture from the origin
         # first: side2_pre).  So while capturing, every rank keeps its work
         # on its own stream (the ranks' streams still run side by side), and
-        # the library does not split batches.
+        # the library does not split batches (its automatic setting already
+        # does not under capture; an explicit one is overridden, then
+        # restored).
         hsflow.set_max_streams(1)
         for o in ops_list:
             if hasattr(o, "flat"):
@@ -688,7 +691,7 @@ def graphed(solver, I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequen
             u, v = gather_owned(st, p, comm)
     finally:
         if rank_streams:
-            hsflow.set_max_streams(0)
+            hsflow.set_max_streams(prev_split)
             for o in ops_list:
                 if hasattr(o, "flat"):
                     o.flat = False

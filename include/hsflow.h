@@ -169,16 +169,33 @@ int hsflow_set_jacobi_kernel(int k);
  * choice.  Process-wide; not thread-safe against running solves. */
 int hsflow_set_strip_rows(int seg_rows);
 
+/* Segment shape of the K4 streaming passes: 0 = automatic (default:
+ * parallelograms -- each stage covers its own rows once and takes the rows
+ * below the segment from the next segment's exchange slot -- wherever the
+ * segment height allows, rectangles otherwise), 1 = rectangles (each
+ * segment recomputes its neighbours' halo rows), 2 = parallelograms (a
+ * solve whose segment height does not allow them fails with HSFLOW_ERR_ARG).
+ * Results are bit-identical for every choice.  Process-wide; not
+ * thread-safe against running solves. */
+int hsflow_set_strip_segments(int mode);
+
 /* Name of the kernel that runs the full-depth Jacobi passes of a solve of
  * this shape under the current settings ("hs_jacobi_strip_kernel",
  * "hs_jacobi_wg_kernel", "hs_jacobi_kernel" or "hs_jacobi_generic_kernel");
  * a static string.  For profiles and the bench's roofline record. */
 const char *hsflow_jacobi_kernel_name(int rows, int cols, int batch, int window);
 
-/* Batches of >= 2 pairs are split over up to n side streams (forked from and
- * joined back to the caller's stream with events) so that concurrent Jacobi
- * launches overlap.  1 disables; 0 restores the default (2).  Process-wide. */
+/* Batches of >= 2 pairs are split over side streams (forked from and joined
+ * back to the caller's stream with events) so that concurrent Jacobi
+ * launches overlap.  0 = automatic (default): 2 streams for eager calls, no
+ * split while the caller's stream is being captured (on ROCm 7.2 a stream
+ * forked inside a capture from a capturing stream other than the capture's
+ * origin crashes hipStreamEndCapture, and the library cannot tell the
+ * origin apart); n >= 1 = up to n streams always (n >= 2 under capture only
+ * when the caller captures on the origin stream itself).  Process-wide.
+ * hsflow_max_streams returns the current setting. */
 int hsflow_set_max_streams(int n);
+int hsflow_max_streams(void);
 
 /* Stream-ordered download of `bytes` from device memory to pinned host
  * memory (hipHostMalloc / torch pin_memory), issued so the runtime moves it

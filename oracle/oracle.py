@@ -13,7 +13,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libhsoracle.so")
+# HSORACLE_LIB: another build of the same sources (tests/test_sanitizers.py
+# points it at the ASan/UBSan build, oracle/Makefile `asan`)
+_LIB_PATH = os.environ.get("HSORACLE_LIB") or os.path.join(_HERE, "libhsoracle.so")
 _lib = None
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -22,7 +24,7 @@ _u8p = ctypes.POINTER(ctypes.c_uint8)
 
 def build(force: bool = False) -> str:
     if force or not os.path.exists(_LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", _HERE])
+        subprocess.check_call(["make", "-s", "-C", _HERE, os.path.basename(_LIB_PATH)])
     return _LIB_PATH
 
 

@@ -13,6 +13,8 @@ Variants (timing questions about K4's issue limit):
   rawoff    loads and stores with the unclamped row offset r * row_bytes (no
             compare / select per row): the most SALU trimming can give
             (timing only; edge rows read garbage)
+  short     each segment streams KB AR rows less (timing only): what a
+            parallelogram segment's stage-steps cost without its exchange
 `probe` runs 1080p x 8 and 4K x 2 solves (hipGraph replays after a 0.15 s
 pre-warm) with each build in its own process, alternating the order twice,
 and prints Mpix*iter/s per build."""
@@ -38,6 +40,10 @@ PATCHES = {
                 "        return r * row_bytes;"),
                ("                    const int so = sin ? y * row_bytes : (int)0x80000000;",
                 "                    const int so = y * row_bytes; (void)sin;")],
+    # the stream ends KB AR steps early, so no stage works on rows below its
+    # segment (timing only: the last rows of every segment are wrong) -- the
+    # stage-steps of a parallelogram segment without its exchange traffic
+    "short": [("    const int t_last = b - 1 + KB * AR;", "    const int t_last = b - 1;")],
 }
 
 

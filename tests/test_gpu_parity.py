@@ -414,6 +414,56 @@ def test_device_solve_captures_into_a_hip_graph(hs, batch, kernel):
         hs.set_jacobi_kernel(0)
 
 
+@pytest.mark.parametrize("kernel", [0, 2])
+def test_batch_capture_on_a_stream_forked_from_the_origin(hs, kernel):
+    """A batch-3 solve captured on a stream B forked from the capture's
+    origin A (the library's automatic setting does not split batches under
+    capture: on ROCm 7.2 a stream forked from a capturing non-origin stream
+    crashes hipStreamEndCapture, profiles/r04_capture_crash.txt); the replay
+    equals the eager solve bit for bit."""
+    import torch
+    assert hs.max_streams() == 0
+    hs.set_jacobi_kernel(kernel)
+    try:
+        batch, rows, cols = 3, 150, 250
+        pairs = [hs.synth_pair(1700 + k, rows, cols) for k in range(batch)]
+        t0 = torch.stack([torch.from_numpy(p[0]) for p in pairs]).cuda()
+        t1 = torch.stack([torch.from_numpy(p[1]) for p in pairs]).cuda()
+        u = torch.empty_like(t0)
+        v = torch.empty_like(t0)
+        ws = hs.alloc_workspace(rows, cols, batch)
+        hs.flow_device(t0, t1, 5, 40, 1.0, u, v, ws)  # eager, split over side streams
+        torch.cuda.synchronize()
+        ref = (u.clone(), v.clone())
+        g = torch.cuda.CUDAGraph()
+        B = torch.cuda.Stream()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            A = torch.cuda.current_stream()
+            B.wait_stream(A)  # B joins the capture: forked from the origin
+            with torch.cuda.stream(B):
+                hs.flow_device(t0, t1, 5, 40, 1.0, u, v, ws, B)
+            A.wait_stream(B)
+        u.fill_(float("nan"))
+        v.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(u, ref[0]) and torch.equal(v, ref[1])
+    finally:
+        hs.set_jacobi_kernel(0)
+
+
+def test_max_streams_setting_round_trips(hs):
+    """hsflow_max_streams reports hsflow_set_max_streams; max_streams_as
+    restores the caller's setting (row_bands.graphed and the bench use it)."""
+    assert hs.max_streams() == 0
+    with hs.max_streams_as(3):
+        assert hs.max_streams() == 3
+        with hs.max_streams_as(1):
+            assert hs.max_streams() == 1
+        assert hs.max_streams() == 3
+    assert hs.max_streams() == 0
+
+
 def _capture_and_replay(hs, batch):
     import torch
     pairs = [hs.synth_pair(1500 + k, 120, 210) for k in range(batch)]
