@@ -804,6 +804,7 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
     same seeds from the resident leg (frame pairs are independent and K2 is
     bit-identical for any batch, split or blocking depth), so a mis-routed
     or mis-ordered scatter or gather cannot pass."""
+    import numpy as np
     import torch
     import torch.distributed as dist
     import frame_parallel as fp
@@ -818,26 +819,36 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
         # the stream's frames back to back in one device buffer per frame
         # slot (as a decoder writing into one allocation leaves them): a
         # group of consecutive pairs is then a view, not a stacked copy
-        # (frame_parallel.batch_of)
-        A = torch.empty((n, rows, cols), dtype=torch.float32, device=dev)
+        # (frame_parallel.batch_of).  8-bit gray frames, the type the
+        # reference's frames have after main.cpp:13-14: a quarter of f32's
+        # bytes over rank 0's links, and K1 packs the same exact gradients
+        # from them as from the f32 frames of the resident leg (the bitwise
+        # check against it below)
+        A = torch.empty((n, rows, cols), dtype=torch.uint8, device=dev)
         B = torch.empty_like(A)
         for j in range(n):
             a, b = hsflow.synth_pair(1000 + j, rows, cols)
-            A[j].copy_(torch.from_numpy(a))
-            B[j].copy_(torch.from_numpy(b))
+            A[j].copy_(torch.from_numpy(a.astype(np.uint8)))
+            B[j].copy_(torch.from_numpy(b.astype(np.uint8)))
         stream = [(A[j], B[j]) for j in range(n)]
     mine = fp.my_pairs(n, rank, world)
-    # each rank's share in groups of at most 8 pairs: 8 pairs fill the chip,
-    # and a group's planes (~330 MB per pass) partly stay in the 256 MB
-    # Infinity Cache between passes, which 64 pairs in one call (2.6 GB per
-    # pass) do not: one rank solved 64 pairs at 1.27 M Mpix*iter/s in one
-    # call against 1.35 M for 8-pair batches.  N > 1: at least 2 groups, so
-    # group c+1 travels while group c is solved and group c's (u, v) travel
-    # back while group c+1 is solved (frame_parallel.run_stream_pipelined;
-    # scripts/scale_predict.py)
-    chunks = max(2 if world > 1 else 1, -(-len(mine) // 8))
+    # each rank's share in groups (frame_parallel.group_sizes, the same on
+    # every rank): one rank, batches of at most 8 pairs (8 pairs fill the
+    # chip, and a group's planes, ~330 MB per pass, partly stay in the 256 MB
+    # Infinity Cache between passes, which 64 pairs in one call do not: one
+    # rank solved 64 pairs at 1.27 M Mpix*iter/s in one call against 1.35 M
+    # for 8-pair batches); N > 1, the sizes that minimise the pipeline model
+    # (a large first group solves while the next ones arrive, small last
+    # groups keep the exposed return of the last (u, v) short;
+    # frame_parallel.run_stream_pipelined, scripts/scale_predict.py)
+    in_mb, out_mb = 2 * rows * cols / 1e6, 2 * rows * cols * 4 / 1e6
+
+    def sizes(share):
+        return fp.group_sizes(share, world, in_mb, out_mb)
+
+    my_sizes = sizes(len(mine))
     if solve_batch is None:
-        ws = hsflow.alloc_workspace(rows, cols, max(1, -(-len(mine) // chunks)), dev)
+        ws = hsflow.alloc_workspace(rows, cols, max(my_sizes), dev)
 
         def solve_batch(I0, I1):
             return hsflow.flow_device(I0, I1, args.window, iters, args.alpha, workspace=ws)
@@ -845,8 +856,8 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
     out = [None]
 
     def one_pass():
-        out[0] = fp.run_stream_pipelined(stream, n, (rows, cols), torch.float32, solve_batch,
-                                         dev, rank, world, chunks=chunks)
+        out[0] = fp.run_stream_pipelined(stream, n, (rows, cols), torch.uint8, solve_batch,
+                                         dev, rank, world, sizes=sizes)
 
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     warm = None
@@ -854,7 +865,7 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
         # untimed, rank-local clock warm-up: the rank's solve of one group of
         # its own size, no collective inside, so ranks may run different
         # counts (prewarm's rule); the timed passes are unchanged
-        g = max(1, -(-len(mine) // chunks))
+        g = max(my_sizes)
         gen = torch.Generator(device=dev).manual_seed(rank)
         W0, W1 = (torch.rand((g, rows, cols), generator=gen, device=dev) * 255 for _ in "01")
         n_w, t_w = prewarm(lambda: solve_batch(W0, W1), sync)
@@ -866,7 +877,8 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
     elapsed = timed_region(one_pass, sync, steps, 1, world, dev)
     leg = {"pairs_per_s": round(n * steps / elapsed, 2),
            "ms_per_pass": round(elapsed / steps * 1e3, 3), "pairs": n,
-           "groups_per_rank": chunks,
+           "groups_per_rank": len(my_sizes), "group_sizes": my_sizes,
+           "frames": "u8",
            "Mpix_iter_per_s": round(n * steps * rows * cols * iters / elapsed / 1e6, 1),
            "transport": _transport(world, dev),
            "scaling": "strong"}

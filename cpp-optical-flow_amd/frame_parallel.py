@@ -118,6 +118,80 @@ def chunk_split(mine: Sequence[int], chunks: int) -> List[List[int]]:
     return out
 
 
+def size_split(mine: Sequence[int], sizes: Sequence[int]) -> List[List[int]]:
+    """This rank's pairs cut into consecutive groups of the given sizes."""
+    assert sum(sizes) == len(mine) and all(s > 0 for s in sizes), (sizes, len(mine))
+    out, start = [], 0
+    for s in sizes:
+        out.append(list(mine[start:start + s]))
+        start += s
+    return out
+
+
+# ---- group sizes of the pipelined stream (BASELINE config 4) -------------
+# Solve time of a batch of g 1080p pairs (300 iterations, w 5), g = 1..8, on
+# one MI355X (graph-replayed, clocks settled; scripts/scale_predict.py
+# `group_solve_ms`, profiles/r05_scale_prediction.json): small batches
+# leave most of the chip idle, so a pair costs 0.72 ms alone and 0.48 ms in
+# a batch of 8.
+GROUP_SOLVE_MS = (0.725, 1.40, 2.05, 2.70, 2.95, 3.20, 3.50, 3.80)
+# RCCL point-to-point per peer link (one xGMI link each way; an assumption
+# of a third of the link's 153 GB/s, never measured here: DESIGN.md §6)
+LINK_GBPS = 50.0
+
+
+def pipeline_ms(sizes: Sequence[int], in_mb: float, out_mb: float,
+                solve_ms: Sequence[float] = GROUP_SOLVE_MS, link_gbps: float = LINK_GBPS,
+                remote: bool = True) -> float:
+    """Modelled time of one rank's share in groups of `sizes`: group c's
+    frames arrive over the link (all groups posted at once, in order), its
+    solve starts when they have arrived and the previous solve is done, its
+    (u, v) go back over the other direction of the link in order.  in_mb /
+    out_mb: MB per pair each way.  remote = False: rank 0's own share (no
+    transfers)."""
+    arrive = solve_end = home = 0.0
+    for g in sizes:
+        ms = solve_ms[g - 1] if g <= len(solve_ms) else solve_ms[-1] * g / len(solve_ms)
+        if remote:
+            arrive += g * in_mb / link_gbps
+        solve_end = max(arrive, solve_end) + ms
+        home = max(home, solve_end) + (g * out_mb / link_gbps if remote else 0.0)
+    return max(home, solve_end)
+
+
+def _partitions(n: int, cap: int):
+    """Non-increasing sequences of parts <= cap summing to n."""
+    if n == 0:
+        yield ()
+        return
+    for first in range(min(n, cap), 0, -1):
+        for rest in _partitions(n - first, first):
+            yield (first,) + rest
+
+
+def group_sizes(share: int, world: int, in_mb: float, out_mb: float,
+                solve_ms: Sequence[float] = GROUP_SOLVE_MS, link_gbps: float = LINK_GBPS,
+                cap: int = 8) -> List[int]:
+    """Group sizes of a rank's share of the stream (the same on every rank,
+    so each end of a link knows the other's grouping).  One rank: batches of
+    at most `cap` pairs (8 pairs fill the chip; larger batches fall out of
+    the Infinity Cache).  Several ranks: the non-increasing sizes <= cap
+    that minimise pipeline_ms -- a large first group solves efficiently
+    while later groups arrive, small last groups keep the exposed return of
+    the last (u, v) short."""
+    if share <= 0:
+        return []
+    if world == 1:
+        k = -(-share // cap)
+        return [share // k + (1 if c < share % k else 0) for c in range(k)]
+    best = None
+    for sizes in _partitions(share, cap):
+        t = pipeline_ms(sizes, in_mb, out_mb, solve_ms, link_gbps)
+        if best is None or t < best[0] - 1e-9:
+            best = (t, list(sizes))
+    return best[1]
+
+
 def batch_of(frames: Sequence[torch.Tensor], device) -> torch.Tensor:
     """The frames as one (len, rows, cols) batch: a view when they already
     lie back to back in one device buffer (a stream decoded into one
@@ -136,14 +210,17 @@ def batch_of(frames: Sequence[torch.Tensor], device) -> torch.Tensor:
 
 def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, dtype,
                          solve_batch: Callable[[torch.Tensor, torch.Tensor], Pair], device,
-                         rank: int, world: int, chunks: int = 2, gather: bool = True):
+                         rank: int, world: int, chunks: int = 2, gather: bool = True,
+                         sizes: Optional[Callable[[int], Sequence[int]]] = None):
     """run_stream with the transfers overlapped: each rank's share is cut into
-    `chunks` groups; rank 0 posts the scatter of every group at once, a rank
-    solves group c (one batched call) as soon as group c has arrived --
-    group c+1 is still in flight -- and sends group c's (u, v) back while it
-    solves group c+1.  With RCCL every step is stream-ordered: work.wait()
-    makes the compute stream wait on the communicator's stream, so no host
-    blocking until rank 0 collects the result.
+    groups (`sizes(share)` gives their sizes, the same function on every
+    rank; default `chunks` near-equal groups); rank 0 posts the scatter of
+    every group at once, a rank solves group c (one batched call) as soon as
+    group c has arrived -- group c+1 is still in flight -- and sends group
+    c's (u, v) back, one message per plane, while it solves group c+1.  With
+    RCCL every step is stream-ordered: work.wait() makes the compute stream
+    wait on the communicator's stream, so no host blocking until rank 0
+    collects the result.
 
     The point-to-point calls are issued in the same order on both ends of
     every link (all scatter groups, then the gather groups in group order),
@@ -152,18 +229,26 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
     of deadlock: a rank posts its receives for every group before its first
     result send.  (Verified with gloo, world 2 and 3; the
     RCCL schedule runs first on the driver's multi-GPU node.)
+    Frames travel in their own dtype (the bench holds the stream as u8, the
+    type main.cpp:13-14 leaves the frames in: a quarter of f32's bytes).
     Returns rank 0's (u, v) list in stream order (None elsewhere, or when
     gather=False).  Bit-identical to run_stream: only the schedule changes."""
     mine = my_pairs(n_pairs, rank, world)
+
+    def split(r, pairs):
+        if sizes is None:
+            return chunk_split(pairs, chunks)
+        return size_split(pairs, list(sizes(len(pairs))))
+
     if world == 1:
         out: List[Pair] = []
-        for grp in chunk_split(mine, chunks):
+        for grp in split(0, mine):
             I0 = batch_of([stream[j][0] for j in grp], device)
             I1 = batch_of([stream[j][1] for j in grp], device)
             u, v = solve_batch(I0, I1)
             out.extend((u[k], v[k]) for k in range(len(grp)))
         return out if gather else None
-    groups = {r: chunk_split(my_pairs(n_pairs, r, world), chunks) for r in range(world)}
+    groups = {r: split(r, my_pairs(n_pairs, r, world)) for r in range(world)}
     n_groups = max(len(g) for g in groups.values())
     # 1. scatter: every group of every rank posted up front, group-major;
     #    one batch per group holding the sends to EVERY destination, so the
@@ -197,7 +282,8 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
             recv_groups.append((a, b, dist.batch_isend_irecv(ops)))
     # 2. per group: solve, then ship the result (rank 0 posts its receives
     #    of the remote ranks' group c first, so they need not wait behind
-    #    its own solve of group c on the communicator's stream)
+    #    its own solve of group c on the communicator's stream); a group's
+    #    (u, v) travel as two messages, one per plane batch
     result: List[Optional[Pair]] = [None] * n_pairs
     pending = []
     for c in range(n_groups):
@@ -206,12 +292,13 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
             for src in range(1, world):
                 if c >= len(groups[src]):
                     continue
-                for j in groups[src][c]:
-                    u = torch.empty(tuple(shape), dtype=torch.float32, device=device)
-                    v = torch.empty(tuple(shape), dtype=torch.float32, device=device)
-                    ops.append(dist.P2POp(dist.irecv, u, src))
-                    ops.append(dist.P2POp(dist.irecv, v, src))
-                    result[j] = (u, v)
+                grp = groups[src][c]
+                u = torch.empty((len(grp),) + tuple(shape), dtype=torch.float32, device=device)
+                v = torch.empty_like(u)
+                ops.append(dist.P2POp(dist.irecv, u, src))
+                ops.append(dist.P2POp(dist.irecv, v, src))
+                for k, j in enumerate(grp):
+                    result[j] = (u[k], v[k])
             if ops:
                 pending.append((None, None, dist.batch_isend_irecv(ops)))
         if c < len(groups[rank]):
@@ -229,10 +316,7 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
                     result[j] = (u[k], v[k])
             elif gather:
                 u, v = u.contiguous(), v.contiguous()
-                ops = []
-                for k in range(len(grp)):
-                    ops.append(dist.P2POp(dist.isend, u[k], 0))
-                    ops.append(dist.P2POp(dist.isend, v[k], 0))
+                ops = [dist.P2POp(dist.isend, u, 0), dist.P2POp(dist.isend, v, 0)]
                 pending.append((u, v, dist.batch_isend_irecv(ops)))
     if rank == 0:
         for req in scatter_reqs:

@@ -53,7 +53,15 @@ def _worker(rank, world, port, q):
         calls = []
         el = bench.timed_region(lambda: calls.append(1) or (rank and __import__("time").sleep(0.05)),
                                 lambda: None, 3, 2, world, dev)
-        leg = bench.stream_leg("tiny", args, world, rank, dev, solve_batch=_solve_batch)
+        ref = None
+        if rank == 0:
+            # the resident leg's input type: f32 frames of the same seeds
+            from synth_ref import synth_pair
+            ps = [synth_pair(1000 + j, ROWS, COLS) for j in range(N_PAIRS)]
+            ref = _solve_batch(torch.from_numpy(np.stack([p[0] for p in ps])),
+                               torch.from_numpy(np.stack([p[1] for p in ps])))
+        leg = bench.stream_leg("tiny", args, world, rank, dev, solve_batch=_solve_batch,
+                               ref=ref)
         q.put((rank, len(calls), el, leg))
     except Exception as e:  # pragma: no cover
         q.put((rank, None, None, repr(e)))
@@ -61,8 +69,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_bench_n2_timing_and_stream_leg_over_gloo():
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_timing_and_stream_leg_over_gloo(world):
+    """The stream leg over gloo: u8 frames scattered from rank 0, each rank's
+    share in the modelled group sizes, (u, v) gathered one message per plane
+    batch; every gathered pair equals the direct f32 solve bit for bit."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -77,12 +88,15 @@ def test_bench_n2_timing_and_stream_leg_over_gloo():
         p.join(timeout=60)
     for r in range(world):
         assert res[r][0] == 5, res[r]  # warmup 2 + timed 3
-    # max over ranks: both report the slow rank's time (>= 3 x 50 ms)
-    assert res[0][1] == res[1][1] and res[0][1] >= 0.15
+    # max over ranks: every rank reports the slow ranks' time (>= 3 x 50 ms)
+    assert all(res[r][1] == res[0][1] for r in range(world)) and res[0][1] >= 0.15
     leg0, leg1 = res[0][2], res[1][2]
     assert isinstance(leg0, dict), leg0
     assert leg0["gathered"] == N_PAIRS and leg0["finite"] and leg0["transport"] == "gloo (cpu tensors)"
     assert leg0["pairs_per_s"] == leg1["pairs_per_s"] > 0  # max-over-ranks time
+    assert leg0["frames"] == "u8" and sum(leg0["group_sizes"]) == len(range(0, N_PAIRS, world))
+    assert leg0["parity"]["bitwise_vs_resident"] == {"pairs": N_PAIRS, "identical": N_PAIRS}
+    assert leg0["parity"]["ok"]
 
 
 def test_stream_leg_gathers_every_pair_in_order_one_rank():

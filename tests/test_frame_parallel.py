@@ -98,6 +98,11 @@ def _solve_batch(I0, I1):
     return torch.stack(us), torch.stack(vs)
 
 
+def _uneven_sizes(share):
+    """Explicit group sizes, different per share (the bench's are modelled)."""
+    return [share] if share < 2 else [share - 1, 1]
+
+
 def _pipe_worker(rank, world, port, chunks, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -107,9 +112,10 @@ def _pipe_worker(rank, world, port, chunks, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         stream = _stream() if rank == 0 else None
+        sizes = _uneven_sizes if chunks == "sizes" else None
         out = fp.run_stream_pipelined(stream, N_PAIRS, (ROWS, COLS), torch.float32,
                                       _solve_batch, torch.device("cpu"), rank, world,
-                                      chunks=chunks)
+                                      chunks=chunks if sizes is None else 2, sizes=sizes)
         q.put(("ok", [(u.numpy(), v.numpy()) for (u, v) in out]) if rank == 0
               else ("peer", out))
     except Exception as e:  # pragma: no cover
@@ -126,7 +132,8 @@ def test_chunk_split():
     assert sum(fp.chunk_split(list(range(9)), 4), []) == list(range(9))
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 2), (3, 2), (2, 3), (3, 1)])
+@pytest.mark.parametrize("world,chunks", [(2, 2), (3, 2), (2, 3), (3, 1), (2, "sizes"),
+                                          (3, "sizes")])
 def test_pipelined_stream_bit_identical(world, chunks):
     """The overlapped schedule (scatter of every group posted up front, group
     c+1 solved while group c's flows travel back) returns every pair's flow
@@ -149,6 +156,27 @@ def test_pipelined_stream_bit_identical(world, chunks):
     for j, (I0, I1) in enumerate(_stream()):
         u, v = _solve(I0, I1)
         assert np.array_equal(flows[j][0], u.numpy()) and np.array_equal(flows[j][1], v.numpy())
+
+
+def test_group_sizes_model():
+    """frame_parallel.group_sizes: one rank takes batches of <= 8; several
+    ranks take the non-increasing sizes the pipeline model rates best -- never
+    worse than even groups, and a pipeline never beats its solves alone."""
+    assert fp.group_sizes(64, 1, 4.1, 16.6) == [8] * 8
+    assert fp.group_sizes(5, 1, 4.1, 16.6) == [5]
+    assert fp.group_sizes(0, 4, 4.1, 16.6) == []
+    for share in (1, 3, 8, 16, 32):
+        s = fp.group_sizes(share, 8, 4.1, 16.6)
+        assert sum(s) == share and all(0 < g <= 8 for g in s)
+        assert list(s) == sorted(s, reverse=True)
+        t = fp.pipeline_ms(s, 4.1, 16.6)
+        for k in (1, 2, 4):
+            even = [share // k + (1 if c < share % k else 0) for c in range(k) if share // k or c < share % k]
+            if all(0 < g <= 8 for g in even):
+                assert t <= fp.pipeline_ms(even, 4.1, 16.6) + 1e-9
+        assert t >= sum(fp.GROUP_SOLVE_MS[g - 1] for g in s) - 1e-9
+    # u8 frames move a quarter of f32's bytes: the model never gets slower
+    assert fp.pipeline_ms([5, 2, 1], 4.1, 16.6) < fp.pipeline_ms([5, 2, 1], 16.6, 16.6)
 
 
 def test_pipelined_single_rank_groups():
