@@ -27,8 +27,14 @@
 #include "hsflow_internal.h"
 #include "hsflow_pool.h"
 
+#include <sys/mman.h>
+
 #if defined(__x86_64__)
 #include <immintrin.h>
+#endif
+
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23  // Linux 5.14
 #endif
 
 namespace hsflow {
@@ -70,6 +76,27 @@ void widen_rows(const float *src, size_t src_pitch, char *dst, size_t step, int 
         const float *row = src + (size_t)r * src_pitch;
         double *d = (double *)(dst + (size_t)r * step);
         for (int x = 0; x < cols; ++x) d[x] = (double)row[x];
+    }
+}
+
+// Fault in the pages of rows [r0, r1) of a host plane (row step `step`,
+// `row_bytes` written per row) for writing, without changing any byte:
+// MADV_POPULATE_WRITE over the rows' span (the span's gaps and its first and
+// last pages keep their contents), or where the kernel lacks it, one write
+// of 0 per page inside the rows themselves (bytes the call overwrites).
+void prefault_rows(char *base, size_t step, size_t row_bytes, int r0, int r1) {
+    if (r1 <= r0) return;
+    const uintptr_t pg = 4096;
+    const uintptr_t a = (uintptr_t)(base + (size_t)r0 * step) & ~(pg - 1);
+    const uintptr_t e = ((uintptr_t)(base + (size_t)(r1 - 1) * step + row_bytes) + pg - 1) &
+                        ~(pg - 1);
+    if (madvise((void *)a, e - a, MADV_POPULATE_WRITE) == 0) return;
+    for (int r = r0; r < r1; ++r) {
+        char *row = base + (size_t)r * step;
+        for (size_t o = 0; o < row_bytes;) {
+            *(volatile char *)(row + o) = 0;
+            o = (((uintptr_t)(row + o)) | (pg - 1)) + 1 - (uintptr_t)row;
+        }
     }
 }
 
@@ -118,10 +145,23 @@ hipError_t download_planes_pipelined(const float *const *src, void *const *dst, 
         if (e == hipSuccess) e = hipEventRecord(events[i], s);
         if (e != hipSuccess) return e;
     }
-    // work items in chunk order, kSlices row slices per chunk: the pool's
-    // threads all wait for chunk 0, widen it together, then chunk 1, ...
+    // work items: first the destination's pages, faulted in while the
+    // solve still runs (a caller's fresh output -- main.cpp:93 declares
+    // `cv::Mat u, v;` anew for every getFlow -- would otherwise take its
+    // first-touch faults in the widening after the last copy: 6 ms of a
+    // 4K call), then the chunks in order, kSlices row slices each: the
+    // pool's threads all wait for chunk 0, widen it together, then chunk 1
     std::atomic<int> err{(int)hipSuccess};
-    Pool::get().run(total * kSlices, [&](int item) {
+    constexpr int kFault = 8;  // slices per plane
+    const int nfault = n * kFault;
+    Pool::get().run(nfault + total * kSlices, [&](int item) {
+        if (item < nfault) {
+            const int k = item / kFault, sl = item % kFault;
+            prefault_rows((char *)dst[k], step, (size_t)cols * 8, rows * sl / kFault,
+                          rows * (sl + 1) / kFault);
+            return;
+        }
+        item -= nfault;
         const int i = item / kSlices, sl = item % kSlices;
         hipError_t e = hipEventSynchronize(events[i]);
         if (e != hipSuccess) {

@@ -135,6 +135,42 @@ def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk) -> P
                 tuple(bands), chunks, tuple(halos))
 
 
+def fit_plan(rows: int, cols: int, levels: int, world: int, window: int, chunk,
+             overlap: bool = False):
+    """plan() with the chunks asked for where they fit, shorter where they do
+    not: each level's chunk is cut (never below 1) until its halo fits the
+    level's smallest band (twice over for the overlapped schedule, whose
+    edge strips and interior tile the band), and each coarser level's is cut
+    no further than the warm-start rule allows (its halo at least half the
+    finer one's, plus one).  Returns (plan, notes): the notes say what was
+    cut, for the caller to report (bench.py prints them to stderr).  Raises
+    ValueError only when even 1-iteration chunks do not fit."""
+    want = list(level_chunks(chunk, levels))
+    A, AR = anchors(window)
+    reach = max(A, AR, 1)
+    notes = []
+    if world > 1:
+        probe = plan(rows, cols, levels, world, window, 1)  # band geometry only
+        for l in range(levels):
+            rows_l = min(bd.b - bd.a for bd in probe.bands[l])
+            room = rows_l // 2 if overlap else rows_l
+            c = want[l]
+            while c > 1 and (c * reach + ((c * reach) & 1)) > room:
+                c -= 1
+            if c != want[l]:
+                notes.append(f"level {l}: chunk {want[l]} -> {c} (band {rows_l} rows)")
+                want[l] = c
+        # the warm-start rule, finest first: a coarse halo below half the
+        # finer one's is raised back if it fits, else the finer chunk shrinks
+        for l in range(levels - 1):
+            h = [c * reach + ((c * reach) & 1) for c in want]
+            while h[l + 1] < h[l] // 2 + 1 and want[l] > 1:
+                want[l] -= 1
+                h[l] = want[l] * reach + ((want[l] * reach) & 1)
+                notes.append(f"level {l}: chunk -> {want[l]} (coarse halo {h[l + 1]})")
+    return plan(rows, cols, levels, world, window, tuple(want)), notes
+
+
 # --------------------------------------------------------------------- ops
 class DeviceOps:
     """libhsflow on torch CUDA tensors (the product path)."""
@@ -298,14 +334,33 @@ class LocalComm:
 
 class DistComm:
     """torch.distributed point-to-point (RCCL for CUDA tensors under the
-    "nccl" backend; numpy / CPU tensors under "gloo")."""
+    "nccl" backend; numpy / CPU tensors under "gloo").  RCCL orders its work
+    against the CURRENT stream: when the rank's work runs on a stream of its
+    own (DeviceOps(stream=...)), the current stream first waits for it (the
+    sends read rows the last chunk wrote), and after the requests complete
+    the rank's stream waits for the current one (the next chunk rewrites
+    rows the transfer reads or writes)."""
+
+    def __init__(self):
+        self._rank_stream = None
 
     def exchange(self, states: Sequence["RankState"], level: int):
         self.wait(self.start(states, level))
 
+    def _enter(self, states):
+        st = getattr(states[0].ops, "stream", None)
+        self._rank_stream = st
+        if st is not None:
+            import torch
+            torch.cuda.current_stream(st.device).wait_stream(st)
+
     def wait(self, handle):
         for req in handle or ():
             req.wait()
+        st, self._rank_stream = self._rank_stream, None
+        if st is not None:
+            import torch
+            st.wait_stream(torch.cuda.current_stream(st.device))
 
     def start(self, states: Sequence["RankState"], level: int):
         """Post the halo exchange; returns the requests (wait() completes
@@ -314,6 +369,7 @@ class DistComm:
         import torch
         import torch.distributed as dist
         (s,) = states
+        self._enter(states)
         p, r, H = s.plan, s.rank, s.plan.halos[level]
         band = p.bands[level][r]
         ops = []
@@ -339,6 +395,7 @@ class DistComm:
         import torch
         import torch.distributed as dist
         (s,) = states
+        self._enter(states)
         p, r, st = s.plan, s.rank, s.strips
         H = st.H
         ops = []

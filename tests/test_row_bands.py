@@ -119,6 +119,30 @@ def test_local_overlapped_bands_equal_undivided_oracle(world, levels, chunk, win
     assert np.array_equal(u, uo) and np.array_equal(v, vo)
 
 
+def test_fit_plan_cuts_coarse_chunks_to_the_bands():
+    """bench's --chunk 24,48 at 8 ranks: window 5 fits as asked; window 7's
+    level-2 halo (144 rows) does not fit its 134-row bands, so that chunk is
+    cut (and said); the overlapped schedule needs two halos per band, and a
+    coarse level never ends with a halo below half the finer one's."""
+    p, notes = rb.fit_plan(4320, 7680, 3, 8, 5, (24, 48))
+    assert p.chunks == (24, 48, 48) and notes == []
+    p, notes = rb.fit_plan(4320, 7680, 3, 8, 7, (24, 48))
+    assert p.chunks[:2] == (24, 48) and p.chunks[2] < 48 and len(notes) == 1
+    with pytest.raises(ValueError):
+        rb.plan(4320, 7680, 3, 8, 7, (24, 48))
+    p, notes = rb.fit_plan(4320, 7680, 3, 8, 5, (24, 48), overlap=True)
+    assert rb.overlap_ok(p) and notes
+    for w in (3, 5, 7, 9):
+        for ov in (False, True):
+            p, _ = rb.fit_plan(4320, 7680, 3, 8, w, (24, 48), overlap=ov)
+            for l in range(2):
+                assert p.halos[l + 1] >= p.halos[l] // 2 + 1
+            assert not ov or rb.overlap_ok(p)
+    # one rank: nothing to fit
+    p, notes = rb.fit_plan(4320, 7680, 3, 1, 7, 1000)
+    assert p.chunks == (1000,) * 3 and notes == []
+
+
 def test_plan_per_level_chunks():
     """Longer chunks on coarse levels (the bench's 24 / 48): one halo per
     level; a coarse halo shorter than half the finer one is refused (the
