@@ -51,9 +51,7 @@ int g_kb_override = 0;
 int g_kernel_override = 0;
 // K4 rows per segment (hsflow_set_strip_rows): 0 = automatic
 int g_strip_rows = 0;
-// K4 segment shape (hsflow_set_strip_segments): 0 = automatic (parallelogram
-// where the segment height allows it), 1 = rectangles, 2 = parallelograms
-int g_strip_segments = 0;
+
 
 // Kernel and blocking depth of a launch's passes.  K4 (streaming strips)
 // runs the full-depth passes when it is built for the window's default
@@ -122,11 +120,6 @@ struct Workspace {
     uint32_t *gpack;
     float *gx, *gy, *gt, *u2, *v2;
     uint32_t *flags;
-    // K4 parallelogram exchange: per pair hsflow::strip_pg_slots slots and
-    // as many flags (hsflow_strips.hip)
-    float *xch;
-    uint32_t *xflag;
-    size_t xslots;  // per pair
     size_t bytes;
 };
 
@@ -146,9 +139,6 @@ Workspace carve(void *base, int rows, int cols, int batch) {
     w.u2 = (float *)take(n * 4);
     w.v2 = (float *)take(n * 4);
     w.flags = (uint32_t *)take((size_t)batch * 4);
-    w.xslots = hsflow::strip_pg_slots(rows, cols);
-    w.xch = (float *)take(w.xslots * batch * hsflow::strip_pg_slot_bytes());
-    w.xflag = (uint32_t *)take(w.xslots * batch * 4);
     w.bytes = off;
     return w;
 }
@@ -356,18 +346,7 @@ int run_passes(hsflow_ctx *ctx, int rows, int cols, int batch, int window, int i
     a.flags = w.flags;
     a.write_through =
         hsflow::fill_limited(window, kb, strip, rows, cols, fill_batch, strip_rows) ? 1 : 0;
-    // K4 parallelogram segments where the height allows them (identical
-    // bits; the flags are zeroed once per solve, each launch leaves them 0)
-    const bool pg = strip && g_strip_segments == 2 && iters >= kb &&
-                    hsflow::strip_pg_ok(window, kb, strip_rows);
-    if (strip && g_strip_segments == 2 && !pg && iters >= kb)
-        return fail(ctx, HSFLOW_ERR_ARG, "K4 parallelogram segments need whole unroll periods "
-                    "of >= %d rows (segment height %d)", hsflow::kStripPgMinRows, strip_rows);
-    if (pg) {
-        a.xch = w.xch;
-        a.xflag = w.xflag;
-        HIP_TRY(ctx, hipMemsetAsync(w.xflag, 0, w.xslots * batch * 4, s));
-    }
+
     // pass p writes the caller's buffers iff (passes-1-p) is even, so the
     // last pass always lands in (u, v)
     auto dst_is_user = [&](int pass) { return ((passes - 1 - pass) & 1) == 0; };
@@ -450,8 +429,6 @@ int jacobi_sub(hsflow_ctx *ctx, int rows, int cols, int nb, int first, int batch
     sub.u2 = w.u2 + off;
     sub.v2 = w.v2 + off;
     sub.flags = w.flags + first;
-    sub.xch = (float *)((char *)w.xch + w.xslots * first * hsflow::strip_pg_slot_bytes());
-    sub.xflag = w.xflag + w.xslots * first;
     // the split's halves run concurrently: the depth is chosen for the batch
     return run_passes(ctx, rows, cols, nb, window, iters, alpha, warm, maybe_f32, u, v, sub,
                       s, batch);
@@ -754,12 +731,6 @@ int hsflow_set_iters_per_launch(int k) {
 int hsflow_set_jacobi_kernel(int k) {
     if (k != 0 && k != 2 && k != 4) return HSFLOW_ERR_ARG;
     g_kernel_override = k;
-    return HSFLOW_OK;
-}
-
-int hsflow_set_strip_segments(int mode) {
-    if (mode < 0 || mode > 2) return HSFLOW_ERR_ARG;
-    g_strip_segments = mode;
     return HSFLOW_OK;
 }
 

@@ -146,11 +146,23 @@ __device__ __forceinline__ void hsum_c2(float ue, float uo, float ve, float vo, 
 // Per-pixel Jacobi operator in normalised form, set up once per pass
 // (hornSchunck.cpp:63-68 rearranged): s = 1/sqrt(alpha^2 + Ix^2 + Iy^2),
 // X = Ix s, Y = Iy s, T = It s; one column pair (even, odd) at a time.
+// Every multiply-add of the Jacobi arithmetic is an explicit fused
+// multiply-add and every other product and sum a plain operation, so no
+// compiler contraction choice (-ffp-contract, which may differ between two
+// instantiations of the same source) can change a bit: K2, K4 and K4's
+// parallelogram segments all round alike.
+__device__ __forceinline__ float fmaf_x(float a, float b, float c) {
+    return __builtin_fmaf(a, b, c);
+}
+__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) {
+    return __builtin_elementwise_fma(a, b, c);
+}
+
 __device__ __forceinline__ void op_setup(float alpha2, float ixe, float iye, float ite,
                                          float ixo, float iyo, float ito, f2v &X, f2v &Y,
                                          f2v &T) {
-    const float se = __builtin_amdgcn_rsqf(alpha2 + ixe * ixe + iye * iye);
-    const float so = __builtin_amdgcn_rsqf(alpha2 + ixo * ixo + iyo * iyo);
+    const float se = __builtin_amdgcn_rsqf(fmaf_x(iye, iye, fmaf_x(ixe, ixe, alpha2)));
+    const float so = __builtin_amdgcn_rsqf(fmaf_x(iyo, iyo, fmaf_x(ixo, ixo, alpha2)));
     X = f2v{ixe * se, ixo * so};
     Y = f2v{iye * se, iyo * so};
     T = f2v{ite * se, ito * so};
@@ -162,9 +174,9 @@ __device__ __forceinline__ void op_setup(float alpha2, float ixe, float iye, flo
 __device__ __forceinline__ void op_update(f2v su, f2v sv, f2v invv, f2v X, f2v Y, f2v T,
                                           f2v &nu, f2v &nv) {
     const f2v ub = su * invv, vb = sv * invv;
-    const f2v k = X * ub + (Y * vb + T);
-    nu = ub - X * k;
-    nv = vb - Y * k;
+    const f2v k = fma2(X, ub, fma2(Y, vb, T));
+    nu = fma2(-X, k, ub);
+    nv = fma2(-Y, k, vb);
 }
 
 }  // namespace hsflow

@@ -23,11 +23,6 @@ struct JacobiArgs {
     int seg_rows;              // K4 strip kernel: output rows per segment
     int write_through;         // store u', v' write-through (sc1) instead of nt: launches
                                // that do not fill the chip (fill_limited)
-    // K4 parallelogram segments (hsflow_strips.hip): exchange slots and
-    // their flags for the launch's pairs, (pair, segment, strip) order;
-    // nullptr -> rectangle segments
-    float *xch;
-    uint32_t *xflag;
 };
 
 // K1 (+ K1f): packed gradients and flags; the f32 planes for every pair
@@ -51,13 +46,6 @@ hipError_t launch_jacobi_strip(JacobiArgs a, int W, int KB, int seg_rows, hipStr
 int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int *nseg,
                    int *nstrips, int override_rows);
 bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots);
-// K4 parallelogram segments: the segment heights they run with, and the
-// exchange area of one pair (strip_pg_slots slots of strip_pg_slot_bytes,
-// and as many u32 flags, zeroed before a solve's first pass)
-constexpr int kStripPgMinRows = 48;
-bool strip_pg_ok(int W, int KB, int seg_rows);
-size_t strip_pg_slots(int rows, int cols);
-size_t strip_pg_slot_bytes();
 // compute units of the current device (cached per device)
 int device_cus();
 int default_kb(int W);

@@ -42,6 +42,13 @@
 #include "hsflow_internal.h"
 #include "hsflow_device.h"
 
+// no implicit contraction anywhere in K4: the arithmetic's fused
+// multiply-adds are explicit (hsflow_device.h), so every instantiation
+// rounds exactly as K2 does whatever the compiler's contraction choices
+// (a parallelogram-segment variant differed from K2 by 1 ulp in a few rows
+// until they were explicit: scripts/k4pg/README.md)
+#pragma clang fp contract(off)
+
 namespace hsflow {
 
 namespace {
@@ -165,7 +172,7 @@ __device__ __forceinline__ void row_op(float alpha2, const RowIn<G32> &d, f2v &X
         it = f2v{ite, ito};
     }
     const f2v a2 = {alpha2, alpha2};
-    const f2v den = a2 + ix * ix + iy * iy;
+    const f2v den = fma2(iy, iy, fma2(ix, ix, a2));
     const f2v sc = {__builtin_amdgcn_rsqf(den.x), __builtin_amdgcn_rsqf(den.y)};
     X = ix * sc;
     Y = iy * sc;
@@ -182,62 +189,20 @@ __device__ __forceinline__ void hrow(f2v u, f2v v, f2v &hu, f2v &hv) {
 
 }  // namespace
 
-// ---- parallelogram segments (PG): the exchange between vertical neighbours
-// A rectangle segment streams KB (W - 1) rows more than it stores: each
-// stage recomputes the rows its neighbours also compute (1.17x the stage
-// work of an 84-row segment at w = 5 after the fill skip).  A PG segment s
-// (s >= 1) instead lets stage i (1-based) cover rows [a + i AR, b + i AR):
-// its top rows need nothing from above the segment, and the 2 AR rows of
-// stage i - 1 its last rows need from below, [b + (i-1) AR, b + (i+1) AR),
-// are the FIRST valid rows of segment s + 1's stage i - 1.  Segment s + 1
-// produces them in its first 2 AR KB steps and publishes their horizontal
-// sums (the values its own next stage consumes, so the bits are the same);
-// segment s reads them in its last 2 AR KB steps (the "drain").  Every
-// stage then computes exactly its own N rows.  Segment 0 keeps the
-// rectangle's top (its stage rows start above the image); the last segment
-// keeps the rectangle's bottom (rows below the image are zeros).
-// Slot of a (pair, segment, strip): (KB - 1) x 2 AR rows x {u, v} x 64 lanes
-// x 8 bytes, at most 20 KB.  Publication: write-through (sc1) stores, one
-// `s_waitcnt vmcnt(0)`, then a device-scope flag; the consumer polls the
-// flag with device-scope loads, reads the slot with sc1 loads and clears
-// the flag (every flag a launch sets is cleared in the same launch; the
-// host zeroes the flags once per solve against stale workspace bytes).
-// Waves are ordered (pair, strip, segment from the bottom), so a producer
-// is never dispatched after its consumer on the XCD that holds both; the
-// poll is bounded (20 ms of s_memrealtime) so no grid can hang.
-constexpr int kXSlotBytes = 20480;
-constexpr uint64_t kXSpinTicks = 2000000;  // 20 ms at 100 MHz
-
-__device__ __forceinline__ uint32_t flag_load(const uint32_t *f) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t x = lane == 0 ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : 0u;
-    return __builtin_amdgcn_readfirstlane(x);
-}
-
-// Segment body of one (pair, segment, strip): strip columns [c0, c0 + 128),
-// streamed downwards.  Rectangle (PG false, or a pair on the f32-gradient
-// path): output rows [a, b), a = seg N, b = min(rows, a + N).  PG: see above.
-// U = unroll period (multiple of the operator ring KB*AR, of 2 and of D).
-template <int W, int KB, int D, int U, bool X2, bool G32, bool WT, bool PG>
+// Segment body: rows [a, b) of strip columns [c0, c0 + 128) of one pair,
+// streamed downwards.  U = unroll period (multiple of the operator ring
+// KB*AR, of 2 and of D).
+template <int W, int KB, int D, int U, bool X2, bool G32, bool WT>
 __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, int plane_bytes,
-                                           int c0, int seg, long slot) {
+                                           int c0, int a, int b) {
     constexpr int A = W - W / 2 - 1, AR = W / 2;
     static_assert(A == AR, "K4 is built for odd windows");
     constexpr int L = KB * AR;  // operator ring: the rows t - AR .. t - KB AR
     static_assert(U % L == 0 && U % 2 == 0 && U % D == 0, "unroll period");
-    static_assert(!PG || (KB - 1) * 2 * AR * 1024 <= kXSlotBytes, "exchange slot");
     using VS = typename VSOf<W>::type;
     constexpr int HLc = KB * A + ((KB * A) & 1), HRc = KB * AR + ((KB * AR) & 1);
     const int lane = threadIdx.x & 63;
     const int cols = p.cols, rows = p.rows;
-    const int nseg = p.tiles_y;
-    const int a = seg * p.seg_rows;
-    const int b = min(rows, a + p.seg_rows);
-    // PG roles: a segment below this one produces our drain rows; we
-    // produce the drain rows of the segment above
-    const bool consumer = PG && seg + 1 < nseg;
-    const bool producer = PG && seg > 0;
     const int gce = c0 + 2 * lane;  // this lane's even image column
     const bool ce = (unsigned)gce < (unsigned)cols;
     const bool co = (unsigned)(gce + 1) < (unsigned)cols;
@@ -270,23 +235,12 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                                               0x00020000);
     rs.vo = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0, plane_bytes,
                                               0x00020000);
-    // PG exchange slots: ours (stores dropped unless we produce) and the one
-    // of the segment below (loads only when we consume)
-    char *x0 = PG ? (char *)p.xch + slot * kXSlotBytes : nullptr;
-    const __amdgpu_buffer_rsrc_t xs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)x0, 0, producer ? kXSlotBytes : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xn = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(PG ? x0 + (long)p.tiles_x * kXSlotBytes : nullptr), 0,
-        consumer ? kXSlotBytes : 0, 0x00020000);
-    const int xl = lane * 8;
 
     const float alpha2 = p.alpha2;
-    // first and last input row of the stream (even: segment starts are even,
-    // and so is KB A); the output rows [lo, hi)
-    const int t_first = producer ? a : a - KB * A;
-    const int lo = producer ? a + KB * AR : a;
-    const int hi = PG ? (consumer ? min(rows, b + KB * AR) : rows) : b;
-    const int t_last = PG ? max(rows - 1 + KB * AR, t_first + 3 * U - 1) : b - 1 + KB * AR;
+    // first and last input row of the stream (the first is even: segment
+    // starts are even, and so is KB A)
+    const int t_first = a - KB * A;
+    const int t_last = b - 1 + KB * AR;
     // Rows outside the image read 0 through the buffer range check, which
     // covers voffset + soffset (gfx950; scripts/ubench/soffset_range.hip):
     // the row's byte offset goes in soffset, 2^31 for rows above the image
@@ -321,10 +275,6 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
             sv[j] = VS{z, z, z};
         }
     }
-    // PG: the flag of the segment below, loaded one block before the drain
-    uint32_t xflag = 0u;
-    const uint32_t *flag_next = PG ? p.xflag + slot + p.tiles_x : nullptr;
-    const int t_drain = consumer ? b : 1 << 30;
 
     // one unrolled block of U time steps from row tb (even); ROWE: some
     // stage row of the block may lie outside the image (top / bottom
@@ -337,83 +287,24 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // steps: 60 of 648 at w 5, KB 6, N 84.  (Also skipping the operator
     // update of the next 2 AR steps, whose rows are not needed either, gave
     // 1-ulp differences in a segment's first rows on the GPU, not kept.)
-    // DRAIN = d > 0 (PG consumers): the d-th of the last two blocks, step
-    // dk = (d-1) U + k after row b arrived: stage j (0-based) has finished
-    // when dk >= 2 AR (j+1); stage m0 = dk / 2 AR takes its input row from
-    // the exchange slot (m0 >= 1) or from the frames (m0 = 0).
-    static_assert(2 * AR * KB == 2 * U, "the pipeline fill and drain are two blocks each");
-    auto block = [&](int tb, auto rowe_c, auto fill_c, auto drain_c) {
+    static_assert(2 * AR * KB == 2 * U, "the pipeline fill is two blocks");
+    auto block = [&](int tb, auto rowe_c, auto fill_c) {
         constexpr bool ROWE = decltype(rowe_c)::value;
         constexpr int FILL = decltype(fill_c)::value;
-        constexpr int DRAIN = decltype(drain_c)::value;
-        if constexpr (PG && DRAIN == 0) {
-            // the flag of the segment below, a block before it is needed
-            if (tb + U == t_drain) xflag = flag_load(flag_next);
-        }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const int t = tb + k;
-            const int dk = DRAIN > 0 ? (DRAIN - 1) * U + k : -1;  // compile-time
-            const int m0 = DRAIN > 0 ? dk / (2 * AR) : 0;
-            if (DRAIN > 0 && dk == 2 * AR - D) {
-                // the first exchange load is next: wait for the producer
-                if (xflag == 0u) {
-                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                    for (;;) {
-                        __builtin_amdgcn_s_sleep(1);
-                        xflag = flag_load(flag_next);
-                        if (xflag != 0u || __builtin_amdgcn_s_memrealtime() - t0 > kXSpinTicks)
-                            break;
-                    }
-                }
-                asm volatile("" ::: "memory");
-                if (lane == 0)
-                    __hip_atomic_store(const_cast<uint32_t *>(flag_next), 0u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
             // 1. this row's input (loaded D steps ago), then the load of
-            //    step k + D into the freed slot
+            //    row t + D into the freed slot
             const RowIn<G32> cur = buf[k % D];
-            if (DRAIN == 0) {
-                issue(buf[k % D], t + D);
-            } else if constexpr (!G32) {
-                const int dn = dk + D;  // the step the load is for
-                if (dn < 2 * AR) {
-                    issue(buf[k % D], t + D);
-                } else if (dn < 2 * U) {
-                    // the horizontal sums of the exchange row (stage dn / 2 AR - 1)
-                    // in the u, v slots; the gradients while a stage still
-                    // needs the row's operator
-                    const int xo = ((dn / (2 * AR) - 1) * 2 * AR + dn % (2 * AR)) * 1024;
-                    const u2v hx = __builtin_amdgcn_raw_buffer_load_b64(xn, xl, xo, 16);
-                    const u2v hy = __builtin_amdgcn_raw_buffer_load_b64(xn, xl, xo + 512, 16);
-                    buf[k % D].u = f2v{__uint_as_float(hx.x), __uint_as_float(hx.y)};
-                    buf[k % D].v = f2v{__uint_as_float(hy.x), __uint_as_float(hy.y)};
-                    if (dn < KB * AR) {
-                        if constexpr (X2) {
-                            buf[k % D].g =
-                                __builtin_amdgcn_raw_buffer_load_b64(rs.g, ld_e, row_off(t + D), 0);
-                        } else {
-                            buf[k % D].g = u2v{
-                                __builtin_amdgcn_raw_buffer_load_b32(rs.g, ld_e, row_off(t + D), 0),
-                                __builtin_amdgcn_raw_buffer_load_b32(rs.g, ld_o, row_off(t + D), 0)};
-                        }
-                    }
-                }
-            }
+            issue(buf[k % D], t + D);
             // 2. level-0 horizontal sums of row t
-            f2v hu = z, hv = z;
-            if (DRAIN == 0 || m0 == 0) {
-                hrow<W>(cur.u, cur.v, hu, hv);
-            } else {
-                hu = cur.u;
-                hv = cur.v;
-            }
+            f2v hu, hv;
+            hrow<W>(cur.u, cur.v, hu, hv);
             // 3. the stages: stage j (1-based) receives row t - (j-1) AR of
             //    iteration j-1 and updates row t - j AR to iteration j
 #pragma unroll
             for (int j = 0; j < KB; ++j) {
-                if (DRAIN > 0 && j < m0) continue;  // finished (compile-time)
                 const int y = t - (j + 1) * AR;
                 // step within the fill (compile-time after unrolling)
                 const int kf = FILL > 0 ? (FILL - 1) * U + k : 1 << 20;
@@ -439,27 +330,12 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                 }
                 if (j + 1 < KB) {
                     hrow<W>(nu, nv, hu, hv);
-                    if constexpr (PG && FILL > 0) {
-                        // producer: the first 2 AR valid rows of stage j + 1
-                        // (1-based) into our exchange slot (dropped unless we
-                        // produce)
-                        const int q = kf - 2 * AR * (j + 1);
-                        if (q >= 0 && q < 2 * AR) {
-                            const int xo = (j * 2 * AR + q) * 1024;
-                            __builtin_amdgcn_raw_buffer_store_b64(
-                                u2v{__float_as_uint(hu.x), __float_as_uint(hu.y)}, xs, xl, xo,
-                                16);
-                            __builtin_amdgcn_raw_buffer_store_b64(
-                                u2v{__float_as_uint(hv.x), __float_as_uint(hv.y)}, xs, xl,
-                                xo + 512, 16);
-                        }
-                    }
                 } else {
                     // every step issues its two stores (out-of-segment rows
                     // at an out-of-range offset, dropped): the compiler then
                     // counts them in its vmcnt waits, which keep the loads
                     // of the D rows ahead in flight
-                    const bool sin = y >= lo && y < hi;
+                    const bool sin = y >= a && y < b;
                     const int so = sin ? y * row_bytes : (int)0x80000000;
                     const int oe = st_e;
                     // nt, or write-through (sc1) in launches that leave most
@@ -491,9 +367,7 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                 }
             }
             // 4. operator of row t, into the slot stage KB has just read
-            //    (in the drain only while a stage still needs the row)
-            if (DRAIN == 0 || dk < KB * AR)
-                row_op<G32>(alpha2, cur, OX[k % L], OY[k % L], OT[k % L]);
+            row_op<G32>(alpha2, cur, OX[k % L], OY[k % L], OT[k % L]);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -501,50 +375,27 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // run a body without row zeroing (one body per loop: a two-body loop
     // makes the allocator spill); the rarely used variants take one loop
     // (the block's stage rows are [tb - KB AR, tb + U - 1 - AR])
-    // (every stream is at least 3 blocks: N + KB (W - 1) >= 3 U; PG: N >= 3 U)
+    // (every stream is at least 3 blocks: N + KB (W - 1) >= 3 U)
     using F0 = std::integral_constant<int, 0>;
-    using T1 = std::true_type;
     int tb = t_first;
-    block(tb, T1{}, std::integral_constant<int, 1>{}, F0{});
+    block(tb, std::true_type{}, std::integral_constant<int, 1>{});
     tb += U;
-    block(tb, T1{}, std::integral_constant<int, 2>{}, F0{});
+    block(tb, std::true_type{}, std::integral_constant<int, 2>{});
     tb += U;
-    if constexpr (PG) {
-        // one more block, then publish our exchange rows: by now their
-        // write-through stores have landed, so the wait is only for the
-        // loads and stores of the last steps
-        block(tb, T1{}, F0{}, F0{});
-        tb += U;
-        if (producer) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store(p.xflag + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    const int t_end = consumer ? b : t_last + 1;  // consumers: blocks end at b
     if constexpr (X2 && !G32) {
-        for (; tb < t_end && tb - KB * AR < 0; tb += U) block(tb, T1{}, F0{}, F0{});
-        for (; tb < t_end && tb + U - 1 - AR < rows; tb += U) block(tb, std::false_type{}, F0{}, F0{});
+        for (; tb <= t_last && tb - KB * AR < 0; tb += U) block(tb, std::true_type{}, F0{});
+        for (; tb <= t_last && tb + U - 1 - AR < rows; tb += U) block(tb, std::false_type{}, F0{});
     }
-    for (; tb < t_end; tb += U) block(tb, T1{}, F0{}, F0{});
-    if constexpr (PG) {
-        if (consumer) {
-            block(tb, T1{}, F0{}, std::integral_constant<int, 1>{});
-            block(tb + U, T1{}, F0{}, std::integral_constant<int, 2>{});
-        }
-    }
+    for (; tb <= t_last; tb += U) block(tb, std::true_type{}, F0{});
 }
 
 // ---------------------------------------------------------------- kernel
 // One wave per (pair, segment, strip); 64-thread workgroups, 8 per CU (two
-// waves per SIMD: up to 256 VGPRs).  Rectangle segments: logical order
-// pair, segment, strip (strips fastest), so the strips that share halo
-// columns run side by side; the XCD-aware remap gives each XCD a contiguous
-// run of them (its L2 serves the shared halo columns and the rows two
-// segments both read).  PG: pair, strip, segment from the bottom up, so a
-// segment's producer (the one below) precedes it in its XCD's dispatch
-// order, and an XCD's run holds whole strip columns.
-template <int W, int KB, int D, int U, bool WT, bool PG>
+// waves per SIMD: up to 256 VGPRs).  Logical order: pair, segment, strip
+// (strips fastest), so the strips that share halo columns run side by side;
+// the XCD-aware remap gives each XCD a contiguous run of them (its L2
+// serves the shared halo columns and the rows two segments both read).
+template <int W, int KB, int D, int U, bool WT>
 __global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs p) {
     const int nblk = gridDim.x;
     const int lin = blockIdx.x;
@@ -555,34 +406,26 @@ __global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs
     const int pair = logical / per_pair;
     if (pair >= p.batch) return;
     const int r = logical - pair * per_pair;
-    int seg, sx;
-    if constexpr (PG) {
-        sx = r / nseg;
-        seg = nseg - 1 - (r - sx * nseg);
-    } else {
-        seg = r / nstrips;
-        sx = r - seg * nstrips;
-    }
+    const int seg = r / nstrips, sx = r - seg * nstrips;
     constexpr int A = W - W / 2 - 1, AR = W / 2;
     constexpr int HLc = KB * A + ((KB * A) & 1), HRc = KB * AR + ((KB * AR) & 1);
     constexpr int OX = 128 - HLc - HRc;
     const int c0 = sx * OX - HLc;
+    const int a = seg * p.seg_rows;
+    const int b = min(p.rows, a + p.seg_rows);  // segments end inside the image
     const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)p.cols;
     const int plane_bytes = p.rows * p.cols * 4;
-    // exchange / flag slot of this wave (PG)
-    const long slot = ((long)pair * nseg + seg) * nstrips + sx;
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
     if (g32) {
-        // f32-gradient pairs keep the rectangle segments (no exchange)
         if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, true, WT, false>(p, pbase, plane_bytes, c0, seg, slot);
+            strip_body<W, KB, D, U, true, true, WT>(p, pbase, plane_bytes, c0, a, b);
         else
-            strip_body<W, KB, D, U, false, true, WT, false>(p, pbase, plane_bytes, c0, seg, slot);
+            strip_body<W, KB, D, U, false, true, WT>(p, pbase, plane_bytes, c0, a, b);
     } else {
         if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, false, WT, PG>(p, pbase, plane_bytes, c0, seg, slot);
+            strip_body<W, KB, D, U, true, false, WT>(p, pbase, plane_bytes, c0, a, b);
         else
-            strip_body<W, KB, D, U, false, false, WT, PG>(p, pbase, plane_bytes, c0, seg, slot);
+            strip_body<W, KB, D, U, false, false, WT>(p, pbase, plane_bytes, c0, a, b);
     }
 }
 
@@ -592,8 +435,6 @@ template <int W, int KB> struct StripCfg;
 template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };
 template <> struct StripCfg<3, 8> { static constexpr int D = 2, U = 8; };
 }  // namespace
-
-bool strip_pg_ok(int W, int KB, int seg_rows);
 
 bool strip_supported(int W, int KB) { return (W == 5 && KB == 6) || (W == 3 && KB == 8); }
 
@@ -663,58 +504,37 @@ bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
 }
 
 // One K4 pass of `a.batch` pairs in segments of `seg_rows` rows (the
-// caller's choice: strip_seg_rows over every pair in flight).  PG segments
-// when the caller passes an exchange area (a.xch, a.xflag; see strip_pg_ok).
-template <int W, int KB>
-static hipError_t launch_strip_wk(const JacobiArgs &a, dim3 grd, hipStream_t s) {
-    using C = StripCfg<W, KB>;
-    const bool wt = a.write_through != 0, pg = a.xch != nullptr;
-    if (pg) {
-        if (wt)
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<W, KB, C::D, C::U, true, true>), grd,
-                               dim3(64), 0, s, a);
-        else
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<W, KB, C::D, C::U, false, true>), grd,
-                               dim3(64), 0, s, a);
-    } else {
-        if (wt)
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<W, KB, C::D, C::U, true, false>), grd,
-                               dim3(64), 0, s, a);
-        else
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<W, KB, C::D, C::U, false, false>), grd,
-                               dim3(64), 0, s, a);
-    }
-    return hipGetLastError();
-}
-
+// caller's choice: strip_seg_rows over every pair in flight).
 hipError_t launch_jacobi_strip(JacobiArgs a, int W, int KB, int seg_rows, hipStream_t s) {
     int nseg = 0, nstrips = 0;
     a.seg_rows = strip_seg_rows(W, KB, a.rows, a.cols, a.batch, 1, &nseg, &nstrips,
                                 seg_rows > 0 ? seg_rows : 84);
     a.tiles_x = nstrips;
     a.tiles_y = nseg;
-    if (a.xch && !strip_pg_ok(W, KB, a.seg_rows)) return hipErrorInvalidValue;
     const long waves = (long)nstrips * nseg * a.batch;
     if (waves <= 0 || waves > 0x7FFFFFFFL) return hipErrorInvalidValue;
     dim3 grd((unsigned)waves, 1, 1);
-    if (W == 5 && KB == 6) return launch_strip_wk<5, 6>(a, grd, s);
-    if (W == 3 && KB == 8) return launch_strip_wk<3, 8>(a, grd, s);
-    return hipErrorInvalidValue;
+    const bool wt = a.write_through != 0;
+    if (W == 5 && KB == 6) {
+        using C = StripCfg<5, 6>;
+        if (wt)
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U, true>), grd, dim3(64), 0,
+                               s, a);
+        else
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U, false>), grd, dim3(64), 0,
+                               s, a);
+    } else if (W == 3 && KB == 8) {
+        using C = StripCfg<3, 8>;
+        if (wt)
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U, true>), grd, dim3(64), 0,
+                               s, a);
+        else
+            hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U, false>), grd, dim3(64), 0,
+                               s, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
-
-// PG segments need whole unroll periods per segment and at least three of
-// them (the fill's two blocks and the block before the publication)
-bool strip_pg_ok(int W, int KB, int seg_rows) {
-    if (!strip_supported(W, KB)) return false;
-    const int U = (W == 5) ? 12 : 8;
-    return seg_rows >= kStripPgMinRows && seg_rows % U == 0 && seg_rows >= 3 * U;
-}
-
-// Exchange slots and flags a PG launch of one pair can use: segments of at
-// least kStripPgMinRows rows, strips of at least 104 output columns.
-size_t strip_pg_slots(int rows, int cols) {
-    return (size_t)((rows + kStripPgMinRows - 1) / kStripPgMinRows) * (size_t)((cols + 103) / 104);
-}
-size_t strip_pg_slot_bytes() { return kXSlotBytes; }
 
 }  // namespace hsflow

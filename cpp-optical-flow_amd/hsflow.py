@@ -52,7 +52,7 @@ EXPORTS = (
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
     "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
     "hsflow_download_device", "hsflow_jacobi_kernel_name", "hsflow_set_strip_rows",
-    "hsflow_set_strip_segments", "hsflow_max_streams",
+    "hsflow_max_streams",
     "hsflow_flow_multi_release",
 )
 BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
@@ -116,7 +116,6 @@ def lib():
     L.hsflow_max_streams.argtypes = []
     L.hsflow_set_jacobi_kernel.argtypes = [i]
     L.hsflow_set_strip_rows.argtypes = [i]
-    L.hsflow_set_strip_segments.argtypes = [i]
     L.hsflow_jacobi_kernel_name.argtypes = [i, i, i, i]
     L.hsflow_jacobi_kernel_name.restype = ctypes.c_char_p
     L.hsflow_pyramid_level_size.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
@@ -659,12 +658,6 @@ def set_jacobi_kernel(k: int):
 def set_strip_rows(seg_rows: int = 0):
     """K4 rows per segment (0 = automatic); identical bits for any choice."""
     _check(lib().hsflow_set_strip_rows(int(seg_rows)))
-
-
-def set_strip_segments(mode: int = 0):
-    """K4 segment shape: 0 automatic (parallelograms where the height allows),
-    1 rectangles, 2 parallelograms.  Identical bits (A/B and tests only)."""
-    _check(lib().hsflow_set_strip_segments(int(mode)))
 
 
 def jacobi_kernel_name(rows, cols, batch, window) -> str:

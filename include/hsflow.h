@@ -169,16 +169,6 @@ int hsflow_set_jacobi_kernel(int k);
  * choice.  Process-wide; not thread-safe against running solves. */
 int hsflow_set_strip_rows(int seg_rows);
 
-/* Segment shape of the K4 streaming passes: 0 = automatic (default:
- * parallelograms -- each stage covers its own rows once and takes the rows
- * below the segment from the next segment's exchange slot -- wherever the
- * segment height allows, rectangles otherwise), 1 = rectangles (each
- * segment recomputes its neighbours' halo rows), 2 = parallelograms (a
- * solve whose segment height does not allow them fails with HSFLOW_ERR_ARG).
- * Results are bit-identical for every choice.  Process-wide; not
- * thread-safe against running solves. */
-int hsflow_set_strip_segments(int mode);
-
 /* Name of the kernel that runs the full-depth Jacobi passes of a solve of
  * this shape under the current settings ("hs_jacobi_strip_kernel",
  * "hs_jacobi_wg_kernel", "hs_jacobi_kernel" or "hs_jacobi_generic_kernel");

@@ -18,11 +18,18 @@ sys.path.insert(0, os.path.join(ROOT, "cpp-optical-flow_amd"))
 import hsflow  # noqa: E402
 
 SHAPES = (("1080p8", 8, 1080, 1920, 300, 5), ("4k2", 2, 2160, 3840, 500, 5),
-          ("4k1", 1, 2160, 3840, 500, 5), ("1080p8w3", 8, 1080, 1920, 300, 3))
+          ("4k1", 1, 2160, 3840, 500, 5), ("1080p8w3", 8, 1080, 1920, 300, 3),
+          ("1080p1", 1, 1080, 1920, 300, 5))
+
+
+SEG_ROWS = 0
+KERNEL = 0
 
 
 def graph_for(mode, I0, I1, window, iters, u, v, ws):
     hsflow.set_strip_segments(mode)
+    hsflow.set_strip_rows(SEG_ROWS)
+    hsflow.set_jacobi_kernel(KERNEL)
     try:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -36,6 +43,8 @@ def graph_for(mode, I0, I1, window, iters, u, v, ws):
         return g
     finally:
         hsflow.set_strip_segments(0)
+        hsflow.set_strip_rows(0)
+        hsflow.set_jacobi_kernel(0)
 
 
 def timed(g, steps=20):
@@ -60,7 +69,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--only", type=int, default=0,
+                    help="time one mode only (1 rectangles, 2 parallelograms), for A/Bs "
+                         "in separate processes")
+    ap.add_argument("--seg", type=int, default=0, help="K4 segment rows (0: automatic)")
+    ap.add_argument("--kernel", type=int, default=0, help="hsflow_set_jacobi_kernel")
     args = ap.parse_args()
+    global SEG_ROWS, KERNEL
+    SEG_ROWS, KERNEL = args.seg, args.kernel
     out = {}
     for tag, batch, rows, cols, iters, window in SHAPES:
         if args.shapes and tag not in args.shapes.split(","):
@@ -71,22 +87,30 @@ def main():
         res = {}
         outs = {}
         graphs = {}
-        for mode in (1, 2):
+        modes = (args.only,) if args.only else (1, 2)
+        for mode in modes:
             u = torch.empty((batch, rows, cols), dtype=torch.float32, device="cuda")
             v = torch.empty_like(u)
             ws = hsflow.alloc_workspace(rows, cols, batch)
-            graphs[mode] = (graph_for(mode, I0, I1, window, iters, u, v, ws), u, v)
+            # ws stays referenced: the graph replays into it
+            graphs[mode] = (graph_for(mode, I0, I1, window, iters, u, v, ws), u, v, ws)
             res[mode] = []
         for r in range(args.rounds):
-            for mode in ((1, 2) if r % 2 == 0 else (2, 1)):
-                g, u, v = graphs[mode]
+            for mode in (modes if r % 2 == 0 else modes[::-1]):
+                g, u, v, _ = graphs[mode]
                 u.fill_(float("nan"))
                 v.fill_(float("nan"))
                 res[mode].append(timed(g))
                 outs[mode] = (u.clone(), v.clone())
+        mpx = batch * rows * cols * iters / 1e3
+        if args.only:
+            out[tag] = {"mode": args.only, "ms": [round(x, 4) for x in res[args.only]],
+                        "M": round(mpx / min(res[args.only]) / 1e6, 4),
+                        "u_sum": float(outs[args.only][0].double().sum())}
+            print(tag, json.dumps(out[tag]), flush=True)
+            continue
         same = bool(torch.equal(outs[1][0], outs[2][0]) and torch.equal(outs[1][1], outs[2][1]))
         nd = int((outs[1][0] != outs[2][0]).sum() + (outs[1][1] != outs[2][1]).sum())
-        mpx = batch * rows * cols * iters / 1e3
         out[tag] = {"rect_ms": [round(x, 4) for x in res[1]],
                     "pg_ms": [round(x, 4) for x in res[2]],
                     "rect_M": round(mpx / min(res[1]) / 1e6, 4),
@@ -96,7 +120,7 @@ def main():
                     "finite": bool(torch.isfinite(outs[2][0]).all())}
         print(tag, json.dumps(out[tag]), flush=True)
     print("RESULT " + json.dumps(out), flush=True)
-    return 0 if all(v["bit_identical"] for v in out.values()) else 1
+    return 0 if all(v.get("bit_identical", True) for v in out.values()) else 1
 
 
 if __name__ == "__main__":

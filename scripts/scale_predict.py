@@ -4,15 +4,15 @@ runs are the driver's; DESIGN.md §6 "Predictions" quotes this output).
 
     python scripts/scale_predict.py > profiles/r04_scale_prediction.json
 
-stream leg (configs[3]): 64 1080p pairs held by rank 0; rank r solves pairs
-  r, r + N, ... in 2 groups (one at N = 1); rank 0 sends 2 x 8.3 MB of f32
-  frames per pair to its owner and receives 2 x 8.3 MB of (u, v) back.
-  A rank's share goes in groups of <= 8 pairs (at least 2; bench.stream_leg).
-  Measured: the resident solve time of a 64/N-pair batch and of one group.
-  Modelled: rank 0 sends a group to every rank at once (one batch per
-  group), each link at LINK_GBPS (RCCL point-to-point over xGMI); group c+1
-  travels while group c is solved, group c's (u, v) return while group c+1
-  is solved, the last group's return is exposed.
+stream leg (configs[3]): 64 1080p pairs held by rank 0 as u8 frames; rank r
+  solves pairs r, r + N, ...; rank 0 sends 2 x 2.07 MB of frames per pair to
+  its owner and receives 2 x 8.3 MB of (u, v) back.  A rank's share goes in
+  the groups frame_parallel.group_sizes picks (bench.stream_leg).
+  Measured: the resident solve time of batches of 1..8 pairs.  Modelled
+  (frame_parallel.pipeline_ms): rank 0 sends a group to every rank at once,
+  each link at LINK_GBPS (RCCL point-to-point over xGMI); group c+1 travels
+  while group c is solved, group c's (u, v) return while later groups are
+  solved, the last group's return is exposed.
 bands leg (configs[4] as stated for N GPUs): one 8K fp16 pair, 3 levels x
   1000 it, rank r solves its extended band in chunks (24 iterations at level
   0, 48 at the coarser levels: bench.py's default) with a halo exchange
@@ -34,10 +34,11 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cpp-optical-flow_amd"), ROOT]
+import frame_parallel as fp  # noqa: E402
 import hsflow  # noqa: E402
 import row_bands as rb  # noqa: E402
 
-LINK_GBPS = 50.0     # RCCL p2p per peer over one xGMI link (~1/3 of the 153 GB/s raw)
+LINK_GBPS = fp.LINK_GBPS  # RCCL p2p per peer over one xGMI link (~1/3 of the 153 GB/s raw)
 XCHG_US = 40.0       # one halo exchange on the critical path (RCCL p2p latency)
 XCHG_HOST_US = 120.0  # host time to post one exchange (clones + batch_isend_irecv)
 
@@ -64,31 +65,33 @@ def resident_ms(batch, reps=6):
     return e0.elapsed_time(e1) / reps
 
 
-def stream_prediction(n, pairs=64):
+def group_solve_ms(reps=6):
+    """Resident solve time of a batch of g 1080p pairs, g = 1..8 (the table
+    frame_parallel.GROUP_SOLVE_MS restates)."""
+    return [round(resident_ms(g, reps), 4) for g in range(1, 9)]
+
+
+def stream_prediction(n, solve_ms, pairs=64):
+    """The stream leg at N ranks: rank 0 keeps pairs 0, N, 2N, ... and sends
+    every other pair's two u8 frames to its owner; each rank's share goes in
+    frame_parallel.group_sizes groups (the bench's rule, with the measured
+    batch solve times); frame_parallel.pipeline_ms models a remote rank's
+    pass (its groups' frames arriving over its link from rank 0, solves,
+    (u, v) back over the other direction), rank 0's own share has no
+    transfers.  The slowest rank sets the pass."""
     per = pairs // n
-    groups = max(2, -(-per // 8)) if n > 1 else 1  # bench.stream_leg
-    t_all = resident_ms(per)
-    t_grp = resident_ms(max(1, per // groups)) if groups > 1 else t_all
-    mb = 2 * 1080 * 1920 * 4 / 1e6  # one direction, one pair
-    remote = pairs - per             # pairs rank 0 does not own
-    # rank 0 sends each group to every rank at once (one batch per group,
-    # frame_parallel.run_stream_pipelined): a group crosses each link in
-    # per/groups pairs' time; group c+1 travels while group c is solved;
-    # group c's (u, v) return while group c+1 is solved
-    grp_link = (per // groups) * mb / LINK_GBPS if n > 1 else 0.0
-    scatter = grp_link * groups
-    gather_grp = grp_link
-    if n == 1:
-        total = t_all
-    else:
-        t = grp_link                          # group 0 arrived
-        for c in range(groups):
-            t = max(t, (c + 1) * grp_link) + t_grp  # group c solved
-        total = t + gather_grp                # the last group's (u, v) home
-    return {"n": n, "pairs_per_rank": per, "groups": groups,
-            "solve_ms_rank_share": round(t_all, 3), "solve_ms_group": round(t_grp, 3),
-            "remote_pairs": remote, "scatter_ms": round(scatter, 3),
-            "gather_ms_per_group": round(gather_grp, 3), "ms_per_pass": round(total, 3),
+    in_mb = 2 * 1080 * 1920 / 1e6        # two u8 frames
+    out_mb = 2 * 1080 * 1920 * 4 / 1e6   # u, v in f32
+    sizes = fp.group_sizes(per, n, in_mb, out_mb, solve_ms, LINK_GBPS)
+    own = fp.group_sizes(per, 1, in_mb, out_mb, solve_ms, LINK_GBPS)
+    t0 = fp.pipeline_ms(own, in_mb, out_mb, solve_ms, LINK_GBPS, remote=False)
+    t0 = fp.pipeline_ms(sizes, in_mb, out_mb, solve_ms, LINK_GBPS, remote=False) \
+        if n > 1 else t0
+    tr = fp.pipeline_ms(sizes, in_mb, out_mb, solve_ms, LINK_GBPS) if n > 1 else 0.0
+    total = max(t0, tr)
+    return {"n": n, "pairs_per_rank": per, "group_sizes": sizes,
+            "rank0_ms": round(t0, 3), "remote_rank_ms": round(tr, 3),
+            "frames": "u8", "ms_per_pass": round(total, 3),
             "pairs_per_s": round(pairs / total * 1e3, 1)}
 
 
@@ -150,7 +153,8 @@ def main():
     res = {"constants": {"LINK_GBPS": LINK_GBPS, "XCHG_US": XCHG_US,
                          "XCHG_HOST_US": XCHG_HOST_US},
            "resident_1080p_x8_ms": round(resident_ms(8), 3)}
-    res["stream"] = [stream_prediction(n) for n in (1, 2, 4, 8)]
+    res["group_solve_ms"] = gs = group_solve_ms()
+    res["stream"] = [stream_prediction(n, gs) for n in (1, 2, 4, 8)]
     res["bands"] = [bands_prediction(n) for n in (1, 2, 4, 8)]
     res["bands_chunk12"] = [bands_prediction(n, 12) for n in (2, 4, 8)]
     print(json.dumps(res, indent=1))
