@@ -33,9 +33,7 @@
 #include <immintrin.h>
 #endif
 
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23  // Linux 5.14
-#endif
+
 
 namespace hsflow {
 
@@ -79,18 +77,27 @@ void widen_rows(const float *src, size_t src_pitch, char *dst, size_t step, int 
     }
 }
 
-// Fault in the pages of rows [r0, r1) of a host plane (row step `step`,
-// `row_bytes` written per row) for writing, without changing any byte:
-// MADV_POPULATE_WRITE over the rows' span (the span's gaps and its first and
-// last pages keep their contents), or where the kernel lacks it, one write
-// of 0 per page inside the rows themselves (bytes the call overwrites).
+// Fresh output planes (main.cpp:93 declares `cv::Mat u, v;` anew for every
+// getFlow) take a first-touch page fault per 4 KB page.  Measured on the GPU
+// box (scripts/pcie/fault_probe.cpp, profiles/r05_fault_probe.txt), for the
+// 132 MB of a 4K pair's two f64 planes: touching every page 18.5 ms on one
+// thread, 8-10 ms on 4-16 (the faults contend); MADV_POPULATE_WRITE 3.3 ms
+// on 4 threads, 6.2 on 8; with MADV_HUGEPAGE first (THP is in `madvise`
+// mode there) the same touches fault 2 MB pages: 1.1-1.4 ms on 8-16 threads.
+// So: advise huge pages over the whole 2 MB extents of each plane's row
+// span (advice only: no byte changes, and memory already resident keeps its
+// pages), then let the pool touch one byte per page inside the rows (bytes
+// the call overwrites) while the device solve runs.
+void advise_hugepages(char *base, size_t step, size_t row_bytes, int rows) {
+    if (rows <= 0) return;
+    const uintptr_t hp = (uintptr_t)2 << 20;
+    const uintptr_t a = ((uintptr_t)base + hp - 1) & ~(hp - 1);
+    const uintptr_t e = ((uintptr_t)(base + (size_t)(rows - 1) * step + row_bytes)) & ~(hp - 1);
+    if (e > a) (void)madvise((void *)a, e - a, MADV_HUGEPAGE);
+}
+
 void prefault_rows(char *base, size_t step, size_t row_bytes, int r0, int r1) {
-    if (r1 <= r0) return;
     const uintptr_t pg = 4096;
-    const uintptr_t a = (uintptr_t)(base + (size_t)r0 * step) & ~(pg - 1);
-    const uintptr_t e = ((uintptr_t)(base + (size_t)(r1 - 1) * step + row_bytes) + pg - 1) &
-                        ~(pg - 1);
-    if (madvise((void *)a, e - a, MADV_POPULATE_WRITE) == 0) return;
     for (int r = r0; r < r1; ++r) {
         char *row = base + (size_t)r * step;
         for (size_t o = 0; o < row_bytes;) {
@@ -152,6 +159,7 @@ hipError_t download_planes_pipelined(const float *const *src, void *const *dst, 
     // 4K call), then the chunks in order, kSlices row slices each: the
     // pool's threads all wait for chunk 0, widen it together, then chunk 1
     std::atomic<int> err{(int)hipSuccess};
+    for (int k = 0; k < n; ++k) advise_hugepages((char *)dst[k], step, (size_t)cols * 8, rows);
     constexpr int kFault = 8;  // slices per plane
     const int nfault = n * kFault;
     Pool::get().run(nfault + total * kSlices, [&](int item) {
