@@ -39,7 +39,7 @@ for sl in range(2):
     cur.wait_stream(cap)
     torch.cuda.synchronize(dev)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+    with hsflow.max_streams_as(2), torch.cuda.graph(g, capture_error_mode="thread_local"):
         hsflow.flow_device(d_in[sl][0], d_in[sl][1], 5, iters, 1.0, d_out[sl][0], d_out[sl][1],
                            ws[sl], torch.cuda.current_stream(dev))
     graphs.append(g)

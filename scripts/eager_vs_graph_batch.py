@@ -40,7 +40,7 @@ for rows, cols, iters, batch in ((1080, 1920, 300, 8), (2160, 3840, 500, 2), (10
     torch.cuda.synchronize()
     ref = u.clone()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+    with hsflow.max_streams_as(2), torch.cuda.graph(g, capture_error_mode="thread_local"):
         hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws, torch.cuda.current_stream())
     n = max(5, int(40 / batch))
     e, gr = [], []

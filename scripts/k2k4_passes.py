@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--f16", action="store_true")
     ap.add_argument("--segments", type=int, default=0,
-                    help="K4 segment shape: 0 automatic, 1 rectangles, 2 parallelograms")
+                    help="K4 segment shape (needs scripts/k4pg/k4_parallelogram.patch): "
+                         "1 rectangles, 2 parallelograms")
     a = ap.parse_args()
     ps = [hsflow.synth_pair(1000 + i, a.rows, a.cols) for i in range(a.batch)]
     I0 = torch.from_numpy(np.stack([p[0] for p in ps])).cuda()
@@ -40,7 +41,8 @@ def main():
     ws = hsflow.alloc_workspace(a.rows, a.cols, a.batch)
     hsflow.set_jacobi_kernel(a.kernel)
     hsflow.set_max_streams(1)
-    hsflow.set_strip_segments(a.segments)
+    if a.segments:
+        hsflow.set_strip_segments(a.segments)
     hsflow.gradients_device(I0, I1, ws)
     for _ in range(a.reps):
         hsflow.jacobi_device(a.rows, a.cols, a.batch, a.window, a.iters, 1.0, u, v, ws)

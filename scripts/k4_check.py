@@ -59,7 +59,7 @@ def timed(kernel, I0, I1, window, iters, reps=5):
         hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws, s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with hsflow.max_streams_as(2), torch.cuda.graph(g):
         hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws,
                            torch.cuda.current_stream())
     for _ in range(2):

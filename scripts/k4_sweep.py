@@ -25,7 +25,7 @@ def timed(I0, I1, window, iters, reps=8):
         hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws, s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with hsflow.max_streams_as(2), torch.cuda.graph(g):
         hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws, torch.cuda.current_stream())
     # the bench's pre-warm: the clocks need ~0.1 s of load to settle
     t = time.perf_counter()

@@ -37,7 +37,7 @@ def graph_for(mode, I0, I1, window, iters, u, v, ws):
             hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws, s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with hsflow.max_streams_as(2), torch.cuda.graph(g, capture_error_mode="thread_local"):
             hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws,
                                torch.cuda.current_stream())
         return g

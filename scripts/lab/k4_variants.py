@@ -87,7 +87,7 @@ for tag, batch, rows, cols, iters in (("1080p8", 8, 1080, 1920, 300), ("4k2", 2,
         hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws, s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+    with hsflow.max_streams_as(2), torch.cuda.graph(g, capture_error_mode="thread_local"):
         hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws, torch.cuda.current_stream())
     t = time.perf_counter(); n = 0
     while time.perf_counter() - t < 0.15:

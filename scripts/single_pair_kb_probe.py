@@ -29,7 +29,7 @@ for rows, cols, iters, window in ((1080, 1920, 300, 5), (720, 1280, 300, 5), (21
         with torch.cuda.stream(s):
             hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws, s)
         torch.cuda.synchronize()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with hsflow.max_streams_as(2), torch.cuda.graph(g, capture_error_mode="thread_local"):
             hsflow.flow_device(I0, I1, window, iters, 1.0, u, v, ws, torch.cuda.current_stream())
         for _ in range(3):
             g.replay()

@@ -47,7 +47,7 @@ def main():
     cur.wait_stream(cap)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+    with hsflow.max_streams_as(2), torch.cuda.graph(g, capture_error_mode="thread_local"):
         hsflow.flow_device(I0, I1, a.window, a.iters, 1.0, u, v, ws,
                            torch.cuda.current_stream())
     torch.cuda.synchronize()
