@@ -130,11 +130,11 @@ def size_split(mine: Sequence[int], sizes: Sequence[int]) -> List[List[int]]:
 
 # ---- group sizes of the pipelined stream (BASELINE config 4) -------------
 # Solve time of a batch of g 1080p pairs (300 iterations, w 5), g = 1..8, on
-# one MI355X (graph-replayed, clocks settled; scripts/scale_predict.py
-# `group_solve_ms`, profiles/r05_scale_prediction.json): small batches
-# leave most of the chip idle, so a pair costs 0.72 ms alone and 0.48 ms in
-# a batch of 8.
-GROUP_SOLVE_MS = (0.725, 1.40, 2.05, 2.70, 2.95, 3.20, 3.50, 3.80)
+# one MI355X (eager calls as the stream leg makes them, clocks settled;
+# scripts/scale_predict.py `group_solve_ms`, profiles/r05_scale_prediction.json):
+# small batches leave most of the chip idle, so a pair costs 0.72 ms alone
+# and 0.47 ms in a batch of 8.
+GROUP_SOLVE_MS = (0.7247, 1.2686, 1.9806, 2.6171, 2.7512, 3.0893, 3.4861, 3.7438)
 # RCCL point-to-point per peer link (one xGMI link each way; an assumption
 # of a third of the link's 153 GB/s, never measured here: DESIGN.md §6)
 LINK_GBPS = 50.0
