@@ -23,6 +23,15 @@ import torch.distributed as dist
 Pair = Tuple[torch.Tensor, torch.Tensor]
 
 
+def _fence(tensors) -> None:
+    """gloo moves CUDA tensors with host code, not in stream order: the
+    stream that wrote them must have finished before they are posted
+    (RCCL is stream-ordered and needs nothing; row_bands.host_transport_fence)."""
+    cuda = [t for t in tensors if isinstance(t, torch.Tensor) and t.is_cuda]
+    if cuda and dist.get_backend() != "nccl":
+        torch.cuda.current_stream(cuda[0].device).synchronize()
+
+
 def owner(j: int, world: int) -> int:
     """Rank that solves pair j (round-robin, weak-scales with world)."""
     return j % world
@@ -49,6 +58,7 @@ def scatter_pairs(stream: Optional[Sequence[Pair]], n_pairs: int, shape, dtype, 
             ops.append(dist.P2POp(dist.isend, I0.to(device).contiguous(), dst))
             ops.append(dist.P2POp(dist.isend, I1.to(device).contiguous(), dst))
         out = [(stream[j][0].to(device), stream[j][1].to(device)) for j in mine]
+        _fence([op.tensor for op in ops])
     else:
         for _ in mine:
             a = torch.empty(shape, dtype=dtype, device=device)
@@ -87,6 +97,7 @@ def gather_flows(flows: List[Pair], n_pairs: int, shape, device, rank: int,
         for (u, v) in flows:
             ops.append(dist.P2POp(dist.isend, u.contiguous(), 0))
             ops.append(dist.P2POp(dist.isend, v.contiguous(), 0))
+        _fence([op.tensor for op in ops])
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
@@ -260,6 +271,7 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
     recv_groups: List[Tuple[torch.Tensor, torch.Tensor, list]] = []
     if rank == 0:
         scatter_reqs = []
+        _fence([stream[0][0]] if stream else [])
         for c in range(n_groups):
             ops = []
             for dst in range(1, world):
@@ -316,6 +328,7 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
                     result[j] = (u[k], v[k])
             elif gather:
                 u, v = u.contiguous(), v.contiguous()
+                _fence([u, v])
                 ops = [dist.P2POp(dist.isend, u, 0), dist.P2POp(dist.isend, v, 0)]
                 pending.append((u, v, dist.batch_isend_irecv(ops)))
     if rank == 0:

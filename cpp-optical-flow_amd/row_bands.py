@@ -332,6 +332,20 @@ class LocalComm:
                 fu[bu.b:bu.b + H] = fd[bd.a:bd.a + H]   # r+1's top rows -> r's bottom halo
 
 
+def host_transport_fence(tensors) -> None:
+    """gloo moves CUDA tensors with host code, not in stream order: before
+    posting, the stream that wrote them must have finished (RCCL -- the
+    "nccl" backend -- is stream-ordered and needs nothing).  Found by the
+    two-process GPU test (tests/test_row_bands.py::
+    test_device_bands_over_gloo_two_processes): without the fence the
+    bands over gloo differed from the single-GPU solve in a few pixels."""
+    import torch
+    import torch.distributed as dist
+    cuda = [t for t in tensors if isinstance(t, torch.Tensor) and t.is_cuda]
+    if cuda and dist.get_backend() != "nccl":
+        torch.cuda.current_stream(cuda[0].device).synchronize()
+
+
 class DistComm:
     """torch.distributed point-to-point (RCCL for CUDA tensors under the
     "nccl" backend; numpy / CPU tensors under "gloo").  RCCL orders its work
@@ -380,6 +394,7 @@ class DistComm:
         # requests before the next chunk rewrites them (under RCCL the wait
         # orders the compute stream after the transfer), so no send copies
         # (the overlapped schedule sends its own buffers, start_strips)
+        host_transport_fence([s.u[level], s.v[level]])
         for f in (s.u[level], s.v[level]):
             if r > 0:
                 ops.append(dist.P2POp(dist.isend, t(f[band.a:band.a + H]), r - 1))
@@ -402,6 +417,7 @@ class DistComm:
 
         def t(x):
             return torch.from_numpy(x) if isinstance(x, np.ndarray) else x
+        host_transport_fence([st.U, st.SU])
         for S, SB in ((st.U, st.SU), (st.V, st.SV)):
             if r > 0:
                 ops.append(dist.P2POp(dist.isend, t(SB[st.top]), r - 1))

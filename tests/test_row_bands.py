@@ -281,6 +281,64 @@ def test_device_overlapped_bands_bit_identical_to_single_gpu(hs, world, levels, 
     assert torch.equal(u, ur) and torch.equal(v, vr)
 
 
+def _device_gloo_worker(rank, world, port, q, shape, levels, iters, chunk):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [here, os.path.join(root, "cpp-optical-flow_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import hsflow
+        rows, cols = shape
+        I0, I1 = hsflow.synth_pair(1000, rows, cols)
+        t0 = torch.from_numpy(I0).cuda().half()
+        t1 = torch.from_numpy(I1).cuda().half()
+        p, _ = rb.fit_plan(rows, cols, levels, world, 5, chunk)
+        comm = rb.DistComm()
+        states = rb.solve([t0], [t1], p, iters, [rb.DeviceOps(5, 1.0, t0.device)], comm, [rank])
+        u, v = rb.gather_owned(states, p, comm)
+        torch.cuda.synchronize()
+        if rank == 0:
+            ur, vr = hsflow.flow_pyramid_device(t0, t1, levels, 5, iters, 1.0)
+            torch.cuda.synchronize()
+            nan = int(torch.isnan(u).sum() + torch.isnan(v).sum())
+            diff = int((u != ur).sum() + (v != vr).sum())
+            q.put(("ok", rank, (nan, diff)))
+        else:
+            q.put(("ok", rank, None))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,levels,iters,chunk", [((540, 960), 3, 200, (24, 48)),
+                                                      ((1080, 1920), 3, 100, (24, 48))])
+def test_device_bands_over_gloo_two_processes(shape, levels, iters, chunk):
+    """bench.py's bands leg path at N = 2: two processes, DistComm over gloo
+    with CUDA tensors (the 2-rank rehearsal's transport; RCCL on a
+    multi-GPU node), DeviceOps on the one GPU; rank 0's gathered (u, v)
+    equal the single-GPU pyramid solve bit for bit."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_device_gloo_worker,
+                         args=(r, world, port, q, shape, levels, iters, chunk))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+    errs = [r for r in res if r[0] == "err"]
+    assert not errs, errs
+    (nan_diff,) = [r[2] for r in res if r[1] == 0]
+    assert nan_diff == (0, 0), nan_diff
+
+
 @pytest.mark.gpu
 def test_device_overlapped_bands_8k_fp16_eight_ranks(hs):
     I0, I1 = hs.synth_pair(1000, 4320, 7680)
