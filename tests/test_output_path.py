@@ -101,3 +101,39 @@ def test_host_call_context_reuse_is_bit_exact(hs):
                 assert np.array_equal(u, ref[0]) and np.array_equal(v, ref[1])
         finally:
             hs.set_jacobi_kernel(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,cols,pad", [(1080, 1920, 64), (270, 480, 3), (2160, 3840, 256)])
+def test_host_call_into_fresh_roi_outputs(hs, rows, cols, pad):
+    """main.cpp:93's fresh `cv::Mat u, v;` -- here as ROIs of larger, freshly
+    mapped private buffers (row step > cols x 8 B): the call faults the
+    output pages in on its copy threads (huge-page advice, one write per
+    page inside the rows) while the solve runs.  The rows get the contiguous
+    call's bits and not one byte between or after them changes."""
+    import mmap
+    import numpy as np
+    a, b = hs.synth_pair(11, rows, cols)
+    a8, b8 = a.astype(np.uint8), b.astype(np.uint8)
+    ctx = hs.Context(0)
+    ru, rv = ctx.flow(a8, b8, 5, 24, 1.0)
+    step_elems = cols + pad
+    planes, maps = [], []
+    for _ in range(2):
+        m = mmap.mmap(-1, (rows + 1) * step_elems * 8, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        big = np.frombuffer(m, np.float64).reshape(rows + 1, step_elems)
+        big[-1, :] = -7.0          # the row after the ROI
+        big[:-1, cols:] = -7.0     # the gaps between ROI rows
+        maps.append(m)
+        planes.append(big)
+    u, v = planes[0][:-1, :cols], planes[1][:-1, :cols]
+    rc = hs.lib().hsflow_flow(ctx._p, a8.ctypes.data, b8.ctypes.data, hs.U8, rows, cols,
+                              a8.strides[0], b8.strides[0], 5, 24, 1.0, u.ctypes.data,
+                              v.ctypes.data, hs.F64, u.strides[0])
+    hs._check(rc, ctx._p)
+    assert np.array_equal(u, ru) and np.array_equal(v, rv)
+    for plane in planes:
+        assert bool((plane[:-1, cols:] == -7.0).all()) and bool((plane[-1, :] == -7.0).all())
+    del u, v, planes, plane, big
+    for m in maps:
+        m.close()
