@@ -104,6 +104,9 @@ PARITY_TOL = 1e-4          # north_star: 1e-4 relative (norm form)
 GOLDEN_JSON = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 GOLDEN_NPZ = os.path.join(ROOT, "tests", "golden", "bench_golden.npz")
 PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r05.json")
+# bands leg: coarse levels up to this many pixels are solved whole on every
+# rank (the 8K pyramid's 1920 x 1080 level 2; row_bands.whole_levels)
+BANDS_WHOLE_MAX_PX = 2_200_000
 KERNEL_SOURCES = ("hsflow_strips.hip", "hsflow_kernels.hip", "hsflow_device.h")
 # measured VALU issue cost per wave64 instruction per SIMD (shader cycles)
 # at each Jacobi kernel's occupancy: profiles/r02_valu_tput.txt, mean of
@@ -1174,7 +1177,11 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     want_overlap = bool(args.overlap if overlap is None else overlap) and world > 1
     # the chunks asked for where their halos fit the bands, shorter where not
     # (e.g. --chunk 24,48 at 8 ranks with window 7); said on stderr
-    p, notes = rb.fit_plan(rows, cols, levels, world, window, chunk, overlap=want_overlap)
+    # coarse levels of at most BANDS_WHOLE_MAX_PX solved whole on every rank:
+    # no chunks, no exchanges (row_bands.whole_levels)
+    whole = rb.whole_levels(rows, cols, levels, world, BANDS_WHOLE_MAX_PX)
+    p, notes = rb.fit_plan(rows, cols, levels, world, window, chunk, overlap=want_overlap,
+                           whole=whole)
     for msg in notes:
         print(f"bench: bands {msg}", file=sys.stderr)
     ops = [ops if ops is not None else rb.DeviceOps(window, alpha, dev)]
@@ -1194,13 +1201,15 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     elapsed = timed_region(one, sync, steps, warmup, world, dev)
     px_all = sum(r * c for r, c in p.sizes)
-    exchanges = sum(-(-iters // c) for c in p.chunks) if world > 1 else 0
+    exchanges = sum(-(-iters // c) for c, w in zip(p.chunks, p.whole) if not w) \
+        if world > 1 else 0
     leg = {"workload": f"{cols}x{rows} {in_dtype}, {levels} levels, {iters} it/level, "
                        f"ws {window}, one pair in {world} row band" + ("s" if world > 1 else ""),
            "value": round(px_all * iters * steps / elapsed / 1e6, 1), "unit": "Mpix*iter/s",
            "ms_per_pair": round(elapsed / steps * 1e3, 3), "steps": steps,
            "pairs_per_s": round(steps / elapsed, 2),
            "n_ranks": world, "chunks_per_level": list(p.chunks),
+           "whole_levels": [l for l, w in enumerate(p.whole) if w],
            "halo_rows_per_level": list(p.halos),
            "exchanges_per_solve": exchanges,
            "exchange": "overlapped with interior iterations" if overlap else "after every chunk",

@@ -63,7 +63,8 @@ class Plan:
     sizes: tuple          # (rows_l, cols_l) per level
     bands: tuple          # bands[l][rank]
     chunks: tuple = ()    # iterations between exchanges, per level
-    halos: tuple = ()     # halo rows, per level
+    halos: tuple = ()     # halo rows, per level (0 on whole levels)
+    whole: tuple = ()     # per level: solved whole on every rank, no exchange
 
 
 def anchors(window: int):
@@ -82,28 +83,38 @@ def level_chunks(chunk, levels: int) -> tuple:
     return (c + (c[-1],) * levels)[:levels]
 
 
-def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk) -> Plan:
+def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk,
+         whole=None) -> Plan:
     """Row bands for every level.  `chunk`: iterations between exchanges,
     one int or one per level (level 0 first; coarse levels have little work
     per chunk, so fewer, longer chunks there cut the exchanges the solve
-    waits on).  Raises ValueError if a band at some level would be shorter
-    than its halo (too many ranks for the image)."""
+    waits on).  `whole`: per level (level 0 first), True = every rank solves
+    that level's whole plane in one call and exchanges nothing (a coarse
+    level small enough that its whole solve costs less than its banded
+    chunks and their exchanges: `whole_levels`); ownership still splits its
+    rows.  Raises ValueError if a band at some level would be shorter than
+    its halo (too many ranks for the image)."""
     if world < 1 or levels < 1:
         raise ValueError("world and levels must be >= 1")
     chunks = level_chunks(chunk, levels)
     if min(chunks) < 1:
         raise ValueError("chunks must be >= 1")
+    whole = tuple(bool(x) for x in (whole or ())) + (False,) * levels
+    whole = tuple(w and world > 1 for w in whole[:levels])
+    if any(whole[l] and not whole[l + 1] for l in range(levels - 1)):
+        raise ValueError("a whole level's coarser levels must be whole too (its warm "
+                         "start reads every coarse row)")
     A, AR = anchors(window)
     halos = []
-    for c in chunks:
-        H = c * max(A, AR, 1)
+    for c, w in zip(chunks, whole):
+        H = 0 if w else c * max(A, AR, 1)
         H += H & 1                  # even: extended bands start on even rows
         halos.append(H)
     # the warm start of level l reads the coarse rows [e0/2, (e1+1)/2) of its
     # extended band, valid after level l+1's last exchange only if the coarse
-    # halo covers them
+    # halo covers them (a whole coarse level has every row)
     for l in range(levels - 1):
-        if world > 1 and halos[l + 1] < halos[l] // 2 + 1:
+        if world > 1 and not whole[l + 1] and halos[l + 1] < halos[l] // 2 + 1:
             raise ValueError(f"level {l + 1}'s halo {halos[l + 1]} cannot cover level {l}'s "
                              f"warm start (halo {halos[l]}): give coarser levels chunks at "
                              "least half as long")
@@ -128,15 +139,33 @@ def plan(rows: int, cols: int, levels: int, world: int, window: int, chunk) -> P
             if world > 1 and b - a < H:
                 raise ValueError(f"level {l}: band {r} has {b - a} rows < halo {H}; "
                                  "use fewer ranks or a shorter chunk")
-            lv.append(Band(a, b, max(0, a - H) if r > 0 else 0,
-                           min(R, b + H) if r < world - 1 else R))
+            if whole[l]:
+                lv.append(Band(a, b, 0, R))
+            else:
+                lv.append(Band(a, b, max(0, a - H) if r > 0 else 0,
+                               min(R, b + H) if r < world - 1 else R))
         bands.append(tuple(lv))
     return Plan(rows, cols, levels, world, window, chunks[0], halos[0], tuple(sizes),
-                tuple(bands), chunks, tuple(halos))
+                tuple(bands), chunks, tuple(halos), whole)
+
+
+def whole_levels(rows: int, cols: int, levels: int, world: int, max_px: int) -> tuple:
+    """The levels (level 0 first) to solve whole on every rank: the coarse
+    ones of at most `max_px` pixels, never level 0, only with several ranks.
+    bench.py takes max_px = 2.2 M: the 8K pyramid's 1920 x 1080 level 2,
+    whose whole solve (2.5 ms for 1000 iterations on one GPU) beats its 21
+    banded chunks and exchanges (3.1-3.3 ms at N = 2..8 by the stated link
+    constants; scripts/scale_predict.py), while the 4K level 1 banded wins
+    from N = 2 on (6.5 ms whole)."""
+    out, r, c = [], rows, cols
+    for l in range(levels):
+        out.append(world > 1 and l > 0 and r * c <= max_px)
+        r, c = (r + 1) // 2, (c + 1) // 2
+    return tuple(out)
 
 
 def fit_plan(rows: int, cols: int, levels: int, world: int, window: int, chunk,
-             overlap: bool = False):
+             overlap: bool = False, whole=None):
     """plan() with the chunks asked for where they fit, shorter where they do
     not: each level's chunk is cut (never below 1) until its halo fits the
     level's smallest band (twice over for the overlapped schedule, whose
@@ -149,9 +178,12 @@ def fit_plan(rows: int, cols: int, levels: int, world: int, window: int, chunk,
     A, AR = anchors(window)
     reach = max(A, AR, 1)
     notes = []
+    wl = tuple(bool(x) for x in (whole or ())) + (False,) * levels
     if world > 1:
         probe = plan(rows, cols, levels, world, window, 1)  # band geometry only
         for l in range(levels):
+            if wl[l]:
+                continue
             rows_l = min(bd.b - bd.a for bd in probe.bands[l])
             room = rows_l // 2 if overlap else rows_l
             c = want[l]
@@ -163,12 +195,14 @@ def fit_plan(rows: int, cols: int, levels: int, world: int, window: int, chunk,
         # the warm-start rule, finest first: a coarse halo below half the
         # finer one's is raised back if it fits, else the finer chunk shrinks
         for l in range(levels - 1):
+            if wl[l + 1]:
+                continue
             h = [c * reach + ((c * reach) & 1) for c in want]
             while h[l + 1] < h[l] // 2 + 1 and want[l] > 1:
                 want[l] -= 1
                 h[l] = want[l] * reach + ((want[l] * reach) & 1)
                 notes.append(f"level {l}: chunk -> {want[l]} (coarse halo {h[l + 1]})")
-    return plan(rows, cols, levels, world, window, tuple(want)), notes
+    return plan(rows, cols, levels, world, window, tuple(want), whole), notes
 
 
 # --------------------------------------------------------------------- ops
@@ -457,15 +491,16 @@ def solve(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Sequence[int]):
                 s.ops.upflow(s.u[l + 1][c0:c1], s.v[l + 1][c0:c1],
                              s.u[l][bd.e0:bd.e1], s.v[l][bd.e0:bd.e1])
             handles.append(s.ops.gradients(s.P0[l][bd.e0:bd.e1], s.P1[l][bd.e0:bd.e1]))
+        whole = bool(p.whole and p.whole[l])
         done = 0
         while True:
-            n = min(p.chunks[l], iters - done)
+            n = (iters - done) if whole else min(p.chunks[l], iters - done)
             if n > 0:
                 for s, h in zip(states, handles):  # each rank owns its ops/workspace
                     bd = p.bands[l][s.rank]
                     s.ops.jacobi(h, s.u[l][bd.e0:bd.e1], s.v[l][bd.e0:bd.e1], n)
                 done += n
-            if p.world > 1:
+            if p.world > 1 and not whole:
                 comm.exchange(states, l)
             if done >= iters:
                 break
@@ -510,7 +545,8 @@ def overlap_ok(p: Plan) -> bool:
     """The overlapped schedule needs every band to hold two halos of rows
     (its edge strips' valid rows and the interior's must tile the band)."""
     return p.world > 1 and all(bd.b - bd.a >= 2 * p.halos[l]
-                               for l, lv in enumerate(p.bands) for bd in lv)
+                               for l, lv in enumerate(p.bands) for bd in lv
+                               if not (p.whole and p.whole[l]))
 
 
 class StripSet:
@@ -647,6 +683,17 @@ def solve_overlapped(I0s, I1s, p: Plan, iters: int, ops_list, comm, ranks: Seque
 
     for l in range(p.levels - 1, -1, -1):
         R, C = p.sizes[l]
+        if p.whole and p.whole[l]:
+            # a whole level: every rank solves its plane in one call
+            for s in states:
+                s.u[l], s.v[l] = s.ops.zeros(R, C), s.ops.zeros(R, C)
+                if l < p.levels - 1:
+                    s.ops.upflow(s.u[l + 1], s.v[l + 1], s.u[l], s.v[l])
+                h = s.ops.gradients(s.P0[l], s.P1[l])
+                s.ops.jacobi(h, s.u[l], s.v[l], iters)
+                if l + 1 < p.levels:
+                    s.u[l + 1] = s.v[l + 1] = None
+            continue
         gi = []
         for s in states:
             bd = p.bands[l][s.rank]

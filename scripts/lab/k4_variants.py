@@ -44,6 +44,14 @@ PATCHES = {
     # segment (timing only: the last rows of every segment are wrong) -- the
     # stage-steps of a parallelogram segment without its exchange traffic
     "short": [("    const int t_last = b - 1 + KB * AR;", "    const int t_last = b - 1;")],
+    # no scheduling barrier between time steps: the scheduler may interleave
+    # step t's later stages with step t+1's earlier ones (more independent
+    # work in flight per wave, more live registers)
+    "nosb": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
+              "        }\n    };")],
+    # a barrier every second step only
+    "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
+             "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
 }
 
 

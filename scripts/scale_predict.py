@@ -123,14 +123,25 @@ def chunk_costs(rows, cols, chunk, nchunks=12):
     return e0.elapsed_time(e1) / nchunks, float(np.median(host)), k1
 
 
-def bands_prediction(n, chunk=(24, 48), iters=1000):
-    p = rb.plan(4320, 7680, 3, n, 5, chunk if n > 1 else iters)
+def bands_prediction(n, chunk=(24, 48), iters=1000, whole_px=2_200_000):
+    """bench.py's plan: per-level chunks, coarse levels of <= whole_px
+    pixels solved whole on every rank (no exchanges)."""
+    whole = rb.whole_levels(4320, 7680, 3, n, whole_px)
+    p = rb.plan(4320, 7680, 3, n, 5, chunk if n > 1 else iters, whole=whole)
     out = {"n": n, "chunks_per_level": list(p.chunks), "halo_rows_per_level": list(p.halos),
            "levels": []}
     total = 0.0
     for l in range(p.levels - 1, -1, -1):
         R, C = p.sizes[l]
         ext = max(b.e1 - b.e0 for b in p.bands[l])
+        if p.whole[l]:  # the whole plane in one call, no exchange
+            g, h, k1 = chunk_costs(ext, C, iters, nchunks=3)
+            nch, lvl = 1, max(g, h) + k1
+            out["levels"].append({"level": l, "band_rows": ext, "cols": C, "chunks": 1,
+                                  "whole": True, "gpu_ms_per_chunk": round(g, 4),
+                                  "host_ms_per_chunk": round(h, 4), "ms": round(lvl, 3)})
+            total += lvl
+            continue
         ck = p.chunks[l]
         g, h, k1 = chunk_costs(ext, C, ck)
         nch = -(-iters // ck)
@@ -156,7 +167,7 @@ def main():
     res["group_solve_ms"] = gs = group_solve_ms()
     res["stream"] = [stream_prediction(n, gs) for n in (1, 2, 4, 8)]
     res["bands"] = [bands_prediction(n) for n in (1, 2, 4, 8)]
-    res["bands_chunk12"] = [bands_prediction(n, 12) for n in (2, 4, 8)]
+    res["bands_no_whole"] = [bands_prediction(n, whole_px=0) for n in (2, 4, 8)]
     print(json.dumps(res, indent=1))
 
 

@@ -143,6 +143,38 @@ def test_fit_plan_cuts_coarse_chunks_to_the_bands():
     assert p.chunks == (1000,) * 3 and notes == []
 
 
+def test_whole_levels_plan():
+    """Coarse levels solved whole on every rank: extended band = the plane,
+    no halo, ownership still split for the gather; a whole level's coarser
+    levels must be whole too; the 8K pyramid at N = 8 takes level 2 whole."""
+    assert rb.whole_levels(4320, 7680, 3, 8, 2_200_000) == (False, False, True)
+    assert rb.whole_levels(4320, 7680, 3, 1, 2_200_000) == (False, False, False)
+    p = rb.plan(400, 522, 3, 3, 5, 6, whole=(False, True, True))
+    for l in (1, 2):
+        R = p.sizes[l][0]
+        assert p.halos[l] == 0
+        assert all(bd.e0 == 0 and bd.e1 == R for bd in p.bands[l])
+        assert [bd.a for bd in p.bands[l]] == sorted(bd.a for bd in p.bands[l])
+        assert p.bands[l][-1].b == R
+    with pytest.raises(ValueError):
+        rb.plan(400, 522, 3, 3, 5, 6, whole=(False, True, False))
+
+
+@pytest.mark.parametrize("world,whole", [(2, (False, True)), (3, (False, True))])
+def test_local_bands_with_whole_levels_equal_undivided_oracle(world, whole):
+    I0, I1 = synth_pair(1000, ROWS, COLS)
+    p = rb.plan(ROWS, COLS, LEVELS, world, 5, CHUNK, whole=whole)
+    for solve in (rb.solve, rb.solve_overlapped):
+        if solve is rb.solve_overlapped and not rb.overlap_ok(p):
+            continue
+        states = solve([I0] * world, [I1] * world, p, ITERS,
+                       [OracleOps(5, 1.0) for _ in range(world)], rb.LocalComm(),
+                       list(range(world)))
+        u, v = rb.gather_owned(states, p, rb.LocalComm())
+        uo, vo = oracle.flow_pyramid(I0, I1, LEVELS, 5, ITERS, 1.0)
+        assert np.array_equal(u, uo) and np.array_equal(v, vo)
+
+
 def test_plan_per_level_chunks():
     """Longer chunks on coarse levels (the bench's 24 / 48): one halo per
     level; a coarse halo shorter than half the finer one is refused (the
@@ -245,12 +277,12 @@ def hs():
 
 
 def _bands_on_one_gpu(hs, I0, I1, levels, window, iters, world, chunk, dtype=None,
-                      overlap=False):
+                      overlap=False, whole=None):
     t0, t1 = torch.from_numpy(I0).cuda(), torch.from_numpy(I1).cuda()
     if dtype is not None:
         t0, t1 = t0.to(dtype), t1.to(dtype)
     rows, cols = I0.shape
-    p = rb.plan(rows, cols, levels, world, window, chunk)
+    p = rb.plan(rows, cols, levels, world, window, chunk, whole=whole)
     ops = [rb.DeviceOps(window, 1.0, t0.device) for _ in range(world)]
     comm = rb.LocalComm()
     solve = rb.solve_overlapped if overlap else rb.solve
@@ -281,7 +313,7 @@ def test_device_overlapped_bands_bit_identical_to_single_gpu(hs, world, levels, 
     assert torch.equal(u, ur) and torch.equal(v, vr)
 
 
-def _device_gloo_worker(rank, world, port, q, shape, levels, iters, chunk):
+def _device_gloo_worker(rank, world, port, q, shape, levels, iters, chunk, whole_px=0):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
@@ -294,7 +326,8 @@ def _device_gloo_worker(rank, world, port, q, shape, levels, iters, chunk):
         I0, I1 = hsflow.synth_pair(1000, rows, cols)
         t0 = torch.from_numpy(I0).cuda().half()
         t1 = torch.from_numpy(I1).cuda().half()
-        p, _ = rb.fit_plan(rows, cols, levels, world, 5, chunk)
+        p, _ = rb.fit_plan(rows, cols, levels, world, 5, chunk,
+                           whole=rb.whole_levels(rows, cols, levels, world, whole_px))
         comm = rb.DistComm()
         states = rb.solve([t0], [t1], p, iters, [rb.DeviceOps(5, 1.0, t0.device)], comm, [rank])
         u, v = rb.gather_owned(states, p, comm)
@@ -314,9 +347,10 @@ def _device_gloo_worker(rank, world, port, q, shape, levels, iters, chunk):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape,levels,iters,chunk", [((540, 960), 3, 200, (24, 48)),
-                                                      ((1080, 1920), 3, 100, (24, 48))])
-def test_device_bands_over_gloo_two_processes(shape, levels, iters, chunk):
+@pytest.mark.parametrize("shape,levels,iters,chunk,whole_px", [
+    ((540, 960), 3, 200, (24, 48), 0), ((1080, 1920), 3, 100, (24, 48), 0),
+    ((1080, 1920), 3, 100, (24, 48), 600_000)])
+def test_device_bands_over_gloo_two_processes(shape, levels, iters, chunk, whole_px):
     """bench.py's bands leg path at N = 2: two processes, DistComm over gloo
     with CUDA tensors (the 2-rank rehearsal's transport; RCCL on a
     multi-GPU node), DeviceOps on the one GPU; rank 0's gathered (u, v)
@@ -326,7 +360,7 @@ def test_device_bands_over_gloo_two_processes(shape, levels, iters, chunk):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_device_gloo_worker,
-                         args=(r, world, port, q, shape, levels, iters, chunk))
+                         args=(r, world, port, q, shape, levels, iters, chunk, whole_px))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -344,6 +378,19 @@ def test_device_overlapped_bands_8k_fp16_eight_ranks(hs):
     I0, I1 = hs.synth_pair(1000, 4320, 7680)
     (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, 3, 5, 30, 8, 12, torch.float16,
                                          overlap=True)
+    assert torch.equal(u, ur) and torch.equal(v, vr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlap", [False, True])
+def test_device_bands_8k_fp16_eight_ranks_whole_coarse_level(hs, overlap):
+    """bench.py's bands plan at N = 8: level 2 (1920 x 1080) solved whole on
+    every rank, levels 1 and 0 banded -- bit-identical to one GPU."""
+    I0, I1 = hs.synth_pair(1000, 4320, 7680)
+    whole = rb.whole_levels(4320, 7680, 3, 8, 2_200_000)
+    assert whole == (False, False, True)
+    (u, v), (ur, vr) = _bands_on_one_gpu(hs, I0, I1, 3, 5, 30, 8, 12, torch.float16,
+                                         overlap=overlap, whole=whole)
     assert torch.equal(u, ur) and torch.equal(v, vr)
 
 
