@@ -1289,7 +1289,7 @@ def host_api_leg(reps=15):
         # (np.empty would reuse glibc's freed chunks below its mmap
         # threshold, i.e. pages already faulted in)
         ts = []
-        for _ in range(max(3, reps // 3)):
+        for _ in range(max(3, reps * 3 // 5)):
             # private anonymous pages, as malloc gives a cv::Mat (mmap.mmap's
             # default MAP_SHARED would be shmem, which faults differently)
             m = mmap.mmap(-1, 2 * rows * cols * 8,
