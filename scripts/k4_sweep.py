@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--kb", type=int, default=0, help="iterations per pass (0 auto)")
     ap.add_argument("--force4", action="store_true", help="K4 even where it does not fill the chip")
+    ap.add_argument("--kernel", type=int, default=0,
+                    help="pass kernel of the k4 columns (4 = K4, 5 = K5; 0 = automatic)")
     a = ap.parse_args()
     cases = {"1080p8": (8, 1080, 1920, 300), "4k2": (2, 2160, 3840, 500),
              "1080p1": (1, 1080, 1920, 300), "4k1": (1, 2160, 3840, 500),
@@ -74,8 +76,8 @@ def main():
         for w in [int(x) for x in a.windows.split(",")]:
             hsflow.set_jacobi_kernel(2)
             t2, u2 = timed(I0, I1, w, iters)
-            hsflow.set_jacobi_kernel(4 if a.force4 else 0)
-            rec = {"tag": a.tag, "kb": a.kb, "streams": a.streams, "case": name, "w": w, "k2_ms": round(t2 * 1e3, 3), "k2": round(mp / t2)}
+            hsflow.set_jacobi_kernel(a.kernel or (4 if a.force4 else 0))
+            rec = {"tag": a.tag, "kernel": a.kernel, "kb": a.kb, "streams": a.streams, "case": name, "w": w, "k2_ms": round(t2 * 1e3, 3), "k2": round(mp / t2)}
             for n in [int(x) for x in a.rows_list.split(",")]:
                 hsflow.set_strip_rows(n)
                 t4, u4 = timed(I0, I1, w, iters)
