@@ -19,11 +19,19 @@ bands leg (configs[4] as stated for N GPUs): one 8K fp16 pair, 3 levels x
   after each.  Measured: per level, the GPU time and
   the host issue time of one chunk on the largest extended band (eager
   jacobi_device calls, as row_bands.solve issues them), K1 per level, the
-  pyramid build.  Modelled: an exchange costs XCHG_US of latency on the
-  critical path (2 x 2 RCCL sends and receives of H rows each, tiny) and the
-  host issues an exchange in XCHG_HOST_US; per chunk the slower of the GPU
-  (chunk + exchange) and the host (issue) sets the pace; the final gather
-  moves the owned rows of (u, v) to rank 0 at LINK_GBPS."""
+  pyramid build.  Modelled: an exchange costs XCHG_US of latency plus its
+  transfer on the critical path (2 x 2 RCCL sends and receives of H rows of
+  u and v each, H x cols x 8 bytes per neighbour at LINK_GBPS, the two
+  neighbours on separate links) and the host issues an exchange in
+  XCHG_HOST_US; per chunk the slower of the GPU (chunk + exchange) and the
+  host (issue) sets the pace; the final gather moves the owned rows of
+  (u, v) to rank 0 at LINK_GBPS.
+  The overlapped schedule (row_bands.solve_overlapped): the middle rank's
+  chunk loop is timed on the GPU with the transfers left out (NullComm),
+  which gives max(host, interior || strips) per chunk; the exchange then
+  only has to land before the strips start: per chunk the slower of that
+  loop (+ XCHG_HOST_US of posting) and XCHG_US + transfer + the strips'
+  GPU time.  The leg runs the cheaper schedule the plan allows."""
 import json
 import os
 import sys
@@ -95,13 +103,14 @@ def stream_prediction(n, solve_ms, pairs=64):
             "pairs_per_s": round(pairs / total * 1e3, 1)}
 
 
-def chunk_costs(rows, cols, chunk, nchunks=12):
-    """GPU ms and host ms of one eager chunk on a rows x cols band."""
-    I0, I1 = hsflow.synth_pair(1000, rows, cols)
-    t0 = torch.from_numpy(I0).cuda().half()
-    t1 = torch.from_numpy(I1).cuda().half()
-    ws = hsflow.alloc_workspace(rows, cols, 1)
-    u = torch.zeros((rows, cols), dtype=torch.float32, device="cuda")
+def chunk_costs(rows, cols, chunk, nchunks=12, batch=1):
+    """GPU ms and host ms of one eager chunk on a rows x cols band (a stack
+    of `batch` such planes)."""
+    ps = [hsflow.synth_pair(1000 + i, rows, cols) for i in range(batch)]
+    t0 = torch.from_numpy(np.stack([p[0] for p in ps])).cuda().half()
+    t1 = torch.from_numpy(np.stack([p[1] for p in ps])).cuda().half()
+    ws = hsflow.alloc_workspace(rows, cols, batch)
+    u = torch.zeros((batch, rows, cols), dtype=torch.float32, device="cuda")
     v = torch.zeros_like(u)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -110,53 +119,134 @@ def chunk_costs(rows, cols, chunk, nchunks=12):
     torch.cuda.synchronize()
     k1 = (time.perf_counter() - k1) * 1e3
     for _ in range(3):
-        hsflow.jacobi_device(rows, cols, 1, 5, chunk, 1.0, u, v, ws, warm_start=True)
+        hsflow.jacobi_device(rows, cols, batch, 5, chunk, 1.0, u, v, ws, warm_start=True)
     torch.cuda.synchronize()
     host = []
     e0.record()
     for _ in range(nchunks):
         h = time.perf_counter()
-        hsflow.jacobi_device(rows, cols, 1, 5, chunk, 1.0, u, v, ws, warm_start=True)
+        hsflow.jacobi_device(rows, cols, batch, 5, chunk, 1.0, u, v, ws, warm_start=True)
         host.append((time.perf_counter() - h) * 1e3)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / nchunks, float(np.median(host)), k1
 
 
-def bands_prediction(n, chunk=(24, 48), iters=1000, whole_px=2_200_000):
-    """bench.py's plan: per-level chunks, coarse levels of <= whole_px
-    pixels solved whole on every rank (no exchanges)."""
+class NullComm:
+    """The exchanges of one rank with the transfers left out: the rank's
+    chunk loop alone (its host issue and its GPU work), for timing."""
+
+    def start(self, states, level):
+        return None
+
+    def wait(self, handle):
+        pass
+
+    def exchange(self, states, level):
+        pass
+
+    def start_strips(self, states):
+        return None
+
+
+def loop_chunk_ms(n, R, C, chunk, overlapped, short=2, long=10, reps=3):
+    """Wall ms per chunk of the middle rank's chunk loop on one level of
+    R x C in N bands (row_bands.solve or solve_overlapped, NullComm): the
+    difference of a long and a short run, so the level's set-up drops out."""
+    p = rb.plan(R, C, 1, n, 5, chunk)
+    if overlapped and not rb.overlap_ok(p):
+        return None
+    a, b = hsflow.synth_pair(1000, R, C)
+    I0 = torch.from_numpy(a).cuda().half()
+    I1 = torch.from_numpy(b).cuda().half()
+    solver = rb.solve_overlapped if overlapped else rb.solve
+    rank = n // 2
+
+    def run(k):
+        ops = rb.DeviceOps(5, 1.0, torch.device("cuda"))
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        solver([I0], [I1], p, k * chunk, [ops], NullComm(), [rank])
+        torch.cuda.synchronize()
+        return time.perf_counter() - t
+
+    run(short)
+    ts = float(np.median([run(short) for _ in range(reps)]))
+    tl = float(np.median([run(long) for _ in range(reps)]))
+    return max(tl - ts, 0.0) / (long - short) * 1e3
+
+
+def _level_plain(n, ext, C, ck, H, iters):
+    g, h, k1 = chunk_costs(ext, C, ck)
+    nch = -(-iters // ck)
+    xfer = H * C * 8 / 1e6 / LINK_GBPS if n > 1 else 0.0  # ms per exchange
+    per = max(g + (XCHG_US / 1e3 + xfer if n > 1 else 0.0),
+              h + (XCHG_HOST_US / 1e3 if n > 1 else 0.0))
+    return nch * per + k1, {"band_rows": ext, "cols": C, "chunks": nch, "chunk": ck,
+                            "halo_rows": H, "gpu_ms_per_chunk": round(g, 4),
+                            "host_ms_per_chunk": round(h, 4),
+                            "exchange_transfer_ms": round(xfer, 4),
+                            "ms_per_chunk": round(per, 4)}
+
+
+def _level_overlapped(n, R, C, ck, H, iters, k1):
+    loop = loop_chunk_ms(n, R, C, ck, True)
+    sg, _, _ = chunk_costs(3 * H, C, ck, batch=2)
+    xfer = H * C * 8 / 1e6 / LINK_GBPS
+    per = max(loop + XCHG_HOST_US / 1e3, XCHG_US / 1e3 + xfer + sg)
+    nch = -(-iters // ck)
+    return nch * per + k1, {"cols": C, "chunks": nch, "chunk": ck, "halo_rows": H,
+                            "loop_ms_per_chunk": round(loop, 4),
+                            "strips_gpu_ms_per_chunk": round(sg, 4),
+                            "exchange_transfer_ms": round(xfer, 4),
+                            "ms_per_chunk": round(per, 4)}
+
+
+def bands_prediction(n, chunk=(24, 48), iters=1000, whole_px=2_200_000, overlap=True):
+    """bench.py's plans (row_bands.fit_plan; coarse levels of <= whole_px
+    pixels solved whole on every rank, no exchanges): the plain schedule,
+    and the overlapped one where its plan allows it; the leg runs the
+    cheaper."""
     whole = rb.whole_levels(4320, 7680, 3, n, whole_px)
-    p = rb.plan(4320, 7680, 3, n, 5, chunk if n > 1 else iters, whole=whole)
-    out = {"n": n, "chunks_per_level": list(p.chunks), "halo_rows_per_level": list(p.halos),
-           "levels": []}
-    total = 0.0
-    for l in range(p.levels - 1, -1, -1):
-        R, C = p.sizes[l]
-        ext = max(b.e1 - b.e0 for b in p.bands[l])
-        if p.whole[l]:  # the whole plane in one call, no exchange
-            g, h, k1 = chunk_costs(ext, C, iters, nchunks=3)
-            nch, lvl = 1, max(g, h) + k1
-            out["levels"].append({"level": l, "band_rows": ext, "cols": C, "chunks": 1,
-                                  "whole": True, "gpu_ms_per_chunk": round(g, 4),
-                                  "host_ms_per_chunk": round(h, 4), "ms": round(lvl, 3)})
-            total += lvl
-            continue
-        ck = p.chunks[l]
-        g, h, k1 = chunk_costs(ext, C, ck)
-        nch = -(-iters // ck)
-        per_chunk = max(g + (XCHG_US / 1e3 if n > 1 else 0.0),
-                        h + (XCHG_HOST_US / 1e3 if n > 1 else 0.0))
-        lvl = nch * per_chunk + k1
-        total += lvl
-        out["levels"].append({"level": l, "band_rows": ext, "cols": C, "chunks": nch,
-                              "gpu_ms_per_chunk": round(g, 4), "host_ms_per_chunk": round(h, 4),
-                              "ms": round(lvl, 3)})
+    out = {"n": n}
+    totals = {}
     own = 4320 // n * 7680 * 8 / 1e6  # MB of (u, v) per remote rank
     gather = own / LINK_GBPS if n > 1 else 0.0
-    total += gather
     out["gather_ms"] = round(gather, 3)
-    out["ms_per_pair"] = round(total, 2)
+    k1s = {}
+    for sched in ("plain", "overlapped"):
+        if sched == "overlapped" and (not overlap or n == 1):
+            continue
+        p, notes = rb.fit_plan(4320, 7680, 3, n, 5, chunk if n > 1 else iters,
+                               overlap=sched == "overlapped", whole=whole)
+        if sched == "overlapped" and not rb.overlap_ok(p):
+            continue
+        rec = {"chunks_per_level": list(p.chunks), "halo_rows_per_level": list(p.halos),
+               "notes": notes, "levels": []}
+        total = gather
+        for l in range(p.levels - 1, -1, -1):
+            R, C = p.sizes[l]
+            ext = max(b.e1 - b.e0 for b in p.bands[l])
+            if p.whole[l]:  # the whole plane in one call, no exchange
+                g, h, k1 = chunk_costs(ext, C, iters, nchunks=3)
+                lvl = max(g, h) + k1
+                rec["levels"].append({"level": l, "band_rows": ext, "cols": C, "whole": True,
+                                      "gpu_ms": round(g, 4), "ms": round(lvl, 3)})
+            elif sched == "plain":
+                lvl, d = _level_plain(n, ext, C, p.chunks[l], p.halos[l], iters)
+                k1s[l] = lvl - d["chunks"] * d["ms_per_chunk"]
+                rec["levels"].append(dict(level=l, ms=round(lvl, 3), **d))
+            else:
+                lvl, d = _level_overlapped(n, R, C, p.chunks[l], p.halos[l], iters,
+                                           k1s.get(l, 0.0))
+                rec["levels"].append(dict(level=l, ms=round(lvl, 3), **d))
+            total += lvl
+        rec["ms_per_pair"] = round(total, 2)
+        out[sched] = rec
+        totals[sched] = total
+    best = min(totals, key=totals.get)
+    out["schedule"] = best
+    out["ms_per_pair"] = round(totals[best], 2)
     return out
 
 
@@ -167,7 +257,7 @@ def main():
     res["group_solve_ms"] = gs = group_solve_ms()
     res["stream"] = [stream_prediction(n, gs) for n in (1, 2, 4, 8)]
     res["bands"] = [bands_prediction(n) for n in (1, 2, 4, 8)]
-    res["bands_no_whole"] = [bands_prediction(n, whole_px=0) for n in (2, 4, 8)]
+    res["bands_no_whole"] = [bands_prediction(n, whole_px=0, overlap=False) for n in (2, 4, 8)]
     print(json.dumps(res, indent=1))
 
 
