@@ -164,12 +164,7 @@ __device__ __forceinline__ void row_op(float alpha2, const RowIn<G32> &d, f2v &X
         iy = d.gy;
         it = d.gt;
     } else {
-        float ixe, iye, ite, ixo, iyo, ito;
-        unpack_grad(d.g.x, ixe, iye, ite);
-        unpack_grad(d.g.y, ixo, iyo, ito);
-        ix = f2v{ixe, ixo};
-        iy = f2v{iye, iyo};
-        it = f2v{ite, ito};
+        unpack_grad_pair(d.g.x, d.g.y, ix, iy, it);
     }
     const f2v a2 = {alpha2, alpha2};
     const f2v den = fma2(iy, iy, fma2(ix, ix, a2));

@@ -15,6 +15,7 @@ Variants (timing questions about K4's issue limit):
             (timing only; edge rows read garbage)
   short     each segment streams KB AR rows less (timing only): what a
             parallelogram segment's stage-steps cost without its exchange
+  oldunpack the per-column v_bfe/v_cvt unpack of the gradients (round 4)
 `probe` runs 1080p x 8 and 4K x 2 solves (hipGraph replays after a 0.15 s
 pre-warm) with each build in its own process, alternating the order twice,
 and prints Mpix*iter/s per build."""
@@ -49,6 +50,14 @@ PATCHES = {
     # work in flight per wave, more live registers)
     "nosb": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
               "        }\n    };")],
+    # round 4's per-column unpack of the packed gradients (v_bfe + v_cvt
+    # for each of the six fields) instead of unpack_grad_pair
+    "oldunpack": [("        unpack_grad_pair(d.g.x, d.g.y, ix, iy, it);",
+                   "        float ixe, iye, ite, ixo, iyo, ito;\n"
+                   "        unpack_grad(d.g.x, ixe, iye, ite);\n"
+                   "        unpack_grad(d.g.y, ixo, iyo, ito);\n"
+                   "        ix = f2v{ixe, ixo};\n        iy = f2v{iye, iyo};\n"
+                   "        it = f2v{ite, ito};")],
     # a barrier every second step only
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
