@@ -783,6 +783,9 @@ int hsflow_flow_device(const void *I0, const void *I1, int dtype_in, int rows, i
                        int batch, int window, int iters, float alpha, float *u, float *v,
                        void *workspace, size_t workspace_bytes, void *stream) {
     DeviceGuard g((hipStream_t)stream);
+    // K1 for the whole batch, then the passes (split over the side streams).
+    // Running each half's K1 on its side stream instead measured 0.6 % slower
+    // (the halves' first passes start out of step; profiles/r05_k1_ab.txt)
     int rc = gradients_impl(nullptr, I0, I1, dtype_in, rows, cols, batch, nullptr,
                             nullptr, nullptr, workspace, workspace_bytes,
                             (hipStream_t)stream);

@@ -80,31 +80,71 @@ __device__ __forceinline__ void sobel_at(const T *a, const T *b, int rows, int c
 // PLANES the planes are written by K1f for the flagged pairs only -- the
 // only pairs whose Jacobi passes read them -- which takes 12 of K1's 24 B
 // per pixel of f32 frames off every solve.
-// block 64 x 4, one pixel per thread; grid (ceil(cols/64), ceil(rows/4), batch)
+// One thread per column pair (c, c + 1) and kK1Rows rows, walking down with
+// the three I0 rows of its 3 x 4 neighbourhood in registers (each row
+// loaded once: 4 I0 and 2 I1 loads per pixel pair and row, against 20 with
+// a pixel per thread re-reading its 3 x 3 window); the arithmetic is
+// sobel_at's, term for term.  Block 64 x 4 threads = 128 columns x 4 kK1Rows
+// rows; grid (ceil(cols/128), ceil(rows/(4 kK1Rows)), batch).
+constexpr int kK1Rows = 8;
 template <typename T, bool PLANES>
 __global__ __launch_bounds__(256) void hs_gradients_kernel(
     const T *__restrict__ I0, const T *__restrict__ I1, int rows, int cols,
     uint32_t *__restrict__ gpack, float *__restrict__ gx, float *__restrict__ gy,
     float *__restrict__ gt, uint32_t *__restrict__ flags) {
     using F = typename GradMath<T>::type;
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    const int r = blockIdx.y * 4 + threadIdx.y;
+    const int c = 2 * (blockIdx.x * 64 + threadIdx.x);
+    const int r0 = (blockIdx.y * 4 + threadIdx.y) * kK1Rows;
     const size_t plane = (size_t)rows * cols;
     bool bad = false;
-    if (r < rows && c < cols) {
-        F dx, dy, dt, z_0, nxt;
-        sobel_at(I0 + blockIdx.z * plane, I1 + blockIdx.z * plane, rows, cols, r, c, dx, dy,
-                 dt, z_0, nxt);
-        const size_t o = blockIdx.z * plane + (size_t)r * cols + c;
-        if constexpr (PLANES) {
-            gx[o] = (float)dx;
-            gy[o] = (float)dy;
-            gt[o] = (float)dt;
+    if (c < cols && r0 < rows) {
+        const T *a = I0 + blockIdx.z * plane, *b = I1 + blockIdx.z * plane;
+        const bool two = c + 1 < cols;
+        // the neighbourhood's columns: c - 1, c, c + 1, c + 2 (reflect-101)
+        const int x0 = reflect101(c - 1, cols), x2 = reflect101(c + 1, cols);
+        const int x3 = reflect101(c + 2, cols);
+        auto ld = [&](int r, F (&q)[4]) {
+            const T *p = a + (size_t)reflect101(r, rows) * cols;
+            q[0] = (F)p[x0];
+            q[1] = (F)p[c];
+            q[2] = (F)p[x2];
+            q[3] = (F)p[x3];
+        };
+        F pm[4], p0[4], pp[4];
+        ld(r0 - 1, pm);
+        ld(r0, p0);
+        const int r1 = min(rows, r0 + kK1Rows);
+        for (int r = r0; r < r1; ++r) {
+            ld(r + 1, pp);
+            const size_t o = blockIdx.z * plane + (size_t)r * cols + c;
+            const T *bn = b + (size_t)r * cols + c;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (k == 1 && !two) break;
+                // column c + k: left k, centre k + 1, right k + 2 of the rows
+                const F m_m = pm[k], m_0 = pm[k + 1], m_p = pm[k + 2];
+                const F z_m = p0[k], z_0 = p0[k + 1], z_p = p0[k + 2];
+                const F p_m = pp[k], p_0 = pp[k + 1], p_p = pp[k + 2];
+                const F nxt = (F)bn[k];
+                const F dx = (m_p - m_m) + (F)2 * (z_p - z_m) + (p_p - p_m);
+                const F dy = (p_m - m_m) + (F)2 * (p_0 - m_0) + (p_p - m_p);
+                const F dt = nxt - z_0;
+                if constexpr (PLANES) {
+                    gx[o + k] = (float)dx;
+                    gy[o + k] = (float)dy;
+                    gt[o + k] = (float)dt;
+                }
+                // packed form is exact iff both frames are integers in [0, 255]
+                bad |= !(z_0 == rint(z_0) && nxt == rint(nxt) && z_0 >= (F)0 &&
+                         z_0 <= (F)255 && nxt >= (F)0 && nxt <= (F)255);
+                gpack[o + k] = pack_grad((int)dx, (int)dy, (int)dt);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pm[k] = p0[k];
+                p0[k] = pp[k];
+            }
         }
-        // packed form is exact iff both frames are integers in [0, 255]
-        bad = !(z_0 == rint(z_0) && nxt == rint(nxt) && z_0 >= (F)0 && z_0 <= (F)255 &&
-                nxt >= (F)0 && nxt <= (F)255);
-        gpack[o] = pack_grad((int)dx, (int)dy, (int)dt);
     }
     if constexpr (std::is_same<T, uint8_t>::value) {
         // 8-bit frames are always integral: the flag is a plain 0, stored
@@ -988,7 +1028,7 @@ template <typename T>
 static void launch_gradients_t(const void *I0, const void *I1, int rows, int cols, int batch,
                                uint32_t *gpack, float *gx, float *gy, float *gt,
                                uint32_t *flags, bool planes, hipStream_t s) {
-    dim3 blk(64, 4, 1), grd((cols + 63) / 64, (rows + 3) / 4, batch);
+    dim3 blk(64, 4, 1), grd((cols + 127) / 128, (rows + 4 * kK1Rows - 1) / (4 * kK1Rows), batch);
     const T *a = (const T *)I0, *b = (const T *)I1;
     if (planes) {
         hipLaunchKernelGGL((hs_gradients_kernel<T, true>), grd, blk, 0, s, a, b, rows, cols,
