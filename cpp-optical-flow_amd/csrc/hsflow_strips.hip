@@ -61,9 +61,11 @@ constexpr int kOOB = 0x7FFFFFF0;
 // M(y-1) + h(y+2) for odd y.  w = 3: Q(t) = h(t) + h(t+1) at even t;
 // S(y) = h(y-1) + Q(y) for even y, Q(y-1) + h(y+1) for odd y.  Rows stream
 // downwards: the arrival of h(t) completes the window of y = t - AR.
-// (An upward stream -- the same sums in the mirrored order, same bits --
-// was built and measured 4 % slower on its own and when passes alternated
-// direction)
+// Segments alternate direction (strip_body's `dir`): upwards the same state
+// machine runs with the row parity flipped (round 3 measured a separately
+// written upward stream 4 % slower; this one shares the downward code, and
+// the alternation makes neighbouring segments read their shared halo rows
+// at the same time -- 4K x 2 +2.1 %, profiles/r05_k4_alt_dir_ab.txt).
 //
 // w = 5.  State before an even arrival t: e0 = h(t-4), e1 = h(t-2),
 // q = Q(t-3), x = h(t-1); before an odd arrival: x = M(t-3).
@@ -189,7 +191,7 @@ __device__ __forceinline__ void hrow(f2v u, f2v v, f2v &hu, f2v &hv) {
 // KB*AR, of 2 and of D).
 template <int W, int KB, int D, int U, bool X2, bool G32, bool WT>
 __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, int plane_bytes,
-                                           int c0, int a, int b) {
+                                           int c0, int a, int b, int dir) {
     constexpr int A = W - W / 2 - 1, AR = W / 2;
     static_assert(A == AR, "K4 is built for odd windows");
     constexpr int L = KB * AR;  // operator ring: the rows t - AR .. t - KB AR
@@ -232,10 +234,18 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                                               0x00020000);
 
     const float alpha2 = p.alpha2;
-    // first and last input row of the stream (the first is even: segment
-    // starts are even, and so is KB A)
-    const int t_first = a - KB * A;
-    const int t_last = b - 1 + KB * AR;
+    // The stream: rows a - KB A .. b - 1 + KB AR, downwards (dir = 1) from
+    // an even first row (segment starts are even, and so is KB A) or upwards
+    // (dir = -1) from an odd first row -- one more row streamed when b - 1 +
+    // KB AR is even.  Upwards the arrival of h(t) completes the window of
+    // t + AR, and K2's parity-ordered sums come out of the same state
+    // machine with the row parity flipped (the adds are commutative, the
+    // association is the same); an odd first row flips the parity of every
+    // arriving row, so the compile-time pattern below serves both
+    // directions.  Step k of a stream always handles the same stage and
+    // ring slots; only row indices depend on the direction.
+    const int t_first = dir > 0 ? a - KB * A : ((b - 1 + KB * AR) | 1);
+    const int nsteps = dir > 0 ? b - a + KB * (A + AR) : t_first - (a - KB * A) + 1;
     // Rows outside the image read 0 through the buffer range check, which
     // covers voffset + soffset (gfx950; scripts/ubench/soffset_range.hip):
     // the row's byte offset goes in soffset, 2^31 for rows above the image
@@ -253,7 +263,7 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
 
     RowIn<G32> buf[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) issue(buf[k], t_first + k);
+    for (int k = 0; k < D; ++k) issue(buf[k], t_first + dir * k);
 
     const f2v z = {0.f, 0.f};
     f2v OX[L], OY[L], OT[L];
@@ -288,11 +298,11 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
         constexpr int FILL = decltype(fill_c)::value;
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            const int t = tb + k;
+            const int t = tb + dir * k;
             // 1. this row's input (loaded D steps ago), then the load of
-            //    row t + D into the freed slot
+            //    the row D steps ahead into the freed slot
             const RowIn<G32> cur = buf[k % D];
-            issue(buf[k % D], t + D);
+            issue(buf[k % D], t + dir * D);
             // 2. level-0 horizontal sums of row t
             f2v hu, hv;
             hrow<W>(cur.u, cur.v, hu, hv);
@@ -300,11 +310,12 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
             //    iteration j-1 and updates row t - j AR to iteration j
 #pragma unroll
             for (int j = 0; j < KB; ++j) {
-                const int y = t - (j + 1) * AR;
+                const int y = t - dir * ((j + 1) * AR);
                 // step within the fill (compile-time after unrolling)
                 const int kf = FILL > 0 ? (FILL - 1) * U + k : 1 << 20;
                 if (kf < 2 * AR * j) break;  // nor any later stage
-                // image-row parity of the arriving row t - j AR (tb even)
+                // image-row parity of the arriving row t - j AR (tb even;
+                // upwards: flipped, tb odd -- the same pattern)
                 const int pt = (k + j * AR) & 1;
                 f2v Su, Sv;
                 if (pt == 0) {
@@ -372,16 +383,24 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // (the block's stage rows are [tb - KB AR, tb + U - 1 - AR])
     // (every stream is at least 3 blocks: N + KB (W - 1) >= 3 U)
     using F0 = std::integral_constant<int, 0>;
-    int tb = t_first;
+    // a block's stage rows: t - dir (j + 1) AR over its U steps and KB stages
+    auto inside = [&](int tb) {
+        const int e = tb + dir * (U - 1);
+        const int lo = dir > 0 ? tb - KB * AR : e + AR;
+        const int hi = dir > 0 ? e - AR : tb + KB * AR;
+        return lo >= 0 && hi < rows;
+    };
+    const int nblk = (nsteps + U - 1) / U;
+    int tb = t_first, ib = 2;
     block(tb, std::true_type{}, std::integral_constant<int, 1>{});
-    tb += U;
+    tb += dir * U;
     block(tb, std::true_type{}, std::integral_constant<int, 2>{});
-    tb += U;
+    tb += dir * U;
     if constexpr (X2 && !G32) {
-        for (; tb <= t_last && tb - KB * AR < 0; tb += U) block(tb, std::true_type{}, F0{});
-        for (; tb <= t_last && tb + U - 1 - AR < rows; tb += U) block(tb, std::false_type{}, F0{});
+        for (; ib < nblk && !inside(tb); tb += dir * U, ++ib) block(tb, std::true_type{}, F0{});
+        for (; ib < nblk && inside(tb); tb += dir * U, ++ib) block(tb, std::false_type{}, F0{});
     }
-    for (; tb <= t_last; tb += U) block(tb, std::true_type{}, F0{});
+    for (; ib < nblk; tb += dir * U, ++ib) block(tb, std::true_type{}, F0{});
 }
 
 // ---------------------------------------------------------------- kernel
@@ -411,16 +430,21 @@ __global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs
     const size_t pbase = (size_t)pair * (size_t)p.rows * (size_t)p.cols;
     const int plane_bytes = p.rows * p.cols * 4;
     const bool g32 = p.flags != nullptr && p.flags[pair] != 0u;
+    // segments alternate direction (even: down, odd: up), so the 2 KB (W - 1)
+    // rows two neighbours share are read by both at their starts (an L2 hit
+    // for one of them) or both at their ends, instead of one at its start
+    // and the other at its end, a whole stream apart
+    const int dir = (seg & 1) ? -1 : 1;
     if (g32) {
         if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, true, WT>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, true, true, WT>(p, pbase, plane_bytes, c0, a, b, dir);
         else
-            strip_body<W, KB, D, U, false, true, WT>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, false, true, WT>(p, pbase, plane_bytes, c0, a, b, dir);
     } else {
         if ((p.cols & 1) == 0)
-            strip_body<W, KB, D, U, true, false, WT>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, true, false, WT>(p, pbase, plane_bytes, c0, a, b, dir);
         else
-            strip_body<W, KB, D, U, false, false, WT>(p, pbase, plane_bytes, c0, a, b);
+            strip_body<W, KB, D, U, false, false, WT>(p, pbase, plane_bytes, c0, a, b, dir);
     }
 }
 

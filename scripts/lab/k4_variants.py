@@ -16,6 +16,8 @@ Variants (timing questions about K4's issue limit):
   short     each segment streams KB AR rows less (timing only): what a
             parallelogram segment's stage-steps cost without its exchange
   oldunpack the per-column v_bfe/v_cvt unpack of the gradients (round 4)
+  haloL2    halo rows read as the nearest segment row (timing only): the
+            cost of the segments' halo re-reads
 `probe` runs 1080p x 8 and 4K x 2 solves (hipGraph replays after a 0.15 s
 pre-warm) with each build in its own process, alternating the order twice,
 and prints Mpix*iter/s per build."""
@@ -58,6 +60,14 @@ PATCHES = {
                    "        unpack_grad(d.g.y, ixo, iyo, ito);\n"
                    "        ix = f2v{ixe, ixo};\n        iy = f2v{iye, iyo};\n"
                    "        it = f2v{ite, ito};")],
+    # timing only: rows outside the segment [a, b) load the nearest segment
+    # row instead (wrong values; the halo rows' HBM/MALL reads become L2
+    # hits of rows the wave just read): what the halo re-read costs, the
+    # most an alternating stream direction could win back
+    "haloL2": [("    auto issue = [&](RowIn<G32> &d, int r) { load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(r)); };",
+                "    auto issue = [&](RowIn<G32> &d, int r) {\n"
+                "        load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(r < a ? a : (r >= b ? b - 1 : r)));\n"
+                "    };")],
     # a barrier every second step only
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
