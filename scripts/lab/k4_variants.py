@@ -18,6 +18,7 @@ Variants (timing questions about K4's issue limit):
   oldunpack the per-column v_bfe/v_cvt unpack of the gradients (round 4)
   haloL2    halo rows read as the nearest segment row (timing only): the
             cost of the segments' halo re-reads
+  d4        4 rows of prefetch instead of 3 at w = 5
 `probe` runs 1080p x 8 and 4K x 2 solves (hipGraph replays after a 0.15 s
 pre-warm) with each build in its own process, alternating the order twice,
 and prints Mpix*iter/s per build."""
@@ -68,6 +69,10 @@ PATCHES = {
                 "    auto issue = [&](RowIn<G32> &d, int r) {\n"
                 "        load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(r < a ? a : (r >= b ? b - 1 : r)));\n"
                 "    };")],
+    # 4 rows of prefetch at w = 5 (the stream's loads run a row further
+    # ahead; +6 VGPRs)
+    "d4": [("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };",
+            "template <> struct StripCfg<5, 6> { static constexpr int D = 4, U = 12; };")],
     # a barrier every second step only
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
