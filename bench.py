@@ -773,12 +773,47 @@ def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
     ok = bool(torch.isfinite(h_out[last][0]).all()) and \
         bool(torch.equal(h_out[last][0], d_out[last][0].cpu())) and \
         bool(torch.equal(h_out[last][1], d_out[last][1].cpu()))
+
+    # each stage of a batch alone on this box (the pipeline's bound is the
+    # slowest of them plus their contention): the upload, the solve, the
+    # download -- box-to-box spread of the e2e rate follows these
+    def alone(fn, reps=5):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    def up():
+        with torch.cuda.stream(s_h2d):
+            d_in[0][0].copy_(host_in[0][0], non_blocking=True)
+            d_in[0][1].copy_(host_in[0][1], non_blocking=True)
+
+    def sv():
+        with torch.cuda.stream(s_cmp):
+            if graphs[0] is not None:
+                graphs[0].replay()
+            else:
+                solve(0, s_cmp)
+
+    def down():
+        hsflow.download_device(h_out[0][0], d_out[0][0], s_d2h)
+        hsflow.download_device(h_out[0][1], d_out[0][1], s_d2h)
+
+    stage_ms = {"h2d": round(alone(up), 3), "solve": round(alone(sv), 3),
+                "d2h": round(alone(down), 3)}
+    mb_in, mb_out = 2 * batch * rows * cols / 1e6, 2 * batch * rows * cols * 4 / 1e6
     return {"pairs_per_s_e2e": round(n_batches * batch / dt, 2),
             "e2e": {"workload": f"{wl_name}, {batch} pairs per batch, {n_batches} batches "
                                 f"({n_batches * batch} pairs)",
                     "input": "pinned host u8 gray frames", "output": "pinned host f32 u, v",
                     "ms_per_batch": round(dt / n_batches * 1e3, 3), "slots": slots,
                     "solve": "hipGraph replay" if graphs[0] is not None else "eager",
+                    "stage_ms_alone": stage_ms,
+                    "link_gbps": {"h2d": round(mb_in / stage_ms["h2d"], 1),
+                                  "d2h": round(mb_out / stage_ms["d2h"], 1)},
                     "finite": ok}}
 
 
