@@ -765,21 +765,20 @@ def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
         run(slots)
         if time.perf_counter() >= t_end:
             break
-    t = time.perf_counter()
-    run(n_batches)
-    dt = time.perf_counter() - t
-    # the last batch's flow arrived intact on the host
-    last = (n_batches - 1) % slots
-    ok = bool(torch.isfinite(h_out[last][0]).all()) and \
-        bool(torch.equal(h_out[last][0], d_out[last][0].cpu())) and \
-        bool(torch.equal(h_out[last][1], d_out[last][1].cpu()))
-
-    # each stage of a batch alone on this box (the pipeline's bound is the
-    # slowest of them plus their contention): the upload, the solve, the
-    # download -- box-to-box spread of the e2e rate follows these
-    def alone(fn, reps=5):
+    # each stage of a batch alone on this box, after the warm-up (the
+    # pipeline's bound is the slowest of them plus their contention): the
+    # upload, the solve, the download -- the box-to-box spread of the e2e
+    # rate follows these
+    def alone(fn, reps=5, warm_s=0.0):
+        # the solve gets the resident legs' pre-warm (the clock needs ~0.1 s
+        # of load to settle: measured cold, the same graph reads 3.98 ms
+        # against 3.6 ms, scripts/e2e_slot_probe.py)
         fn()
         torch.cuda.synchronize(dev)
+        t_end = time.perf_counter() + warm_s
+        while time.perf_counter() < t_end:
+            fn()
+            torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(reps):
             fn()
@@ -802,8 +801,17 @@ def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
         hsflow.download_device(h_out[0][0], d_out[0][0], s_d2h)
         hsflow.download_device(h_out[0][1], d_out[0][1], s_d2h)
 
-    stage_ms = {"h2d": round(alone(up), 3), "solve": round(alone(sv), 3),
+    stage_ms = {"h2d": round(alone(up), 3), "solve": round(alone(sv, warm_s=0.15), 3),
                 "d2h": round(alone(down), 3)}
+    t = time.perf_counter()
+    run(n_batches)
+    dt = time.perf_counter() - t
+    # the last batch's flow arrived intact on the host
+    last = (n_batches - 1) % slots
+    ok = bool(torch.isfinite(h_out[last][0]).all()) and \
+        bool(torch.equal(h_out[last][0], d_out[last][0].cpu())) and \
+        bool(torch.equal(h_out[last][1], d_out[last][1].cpu()))
+
     mb_in, mb_out = 2 * batch * rows * cols / 1e6, 2 * batch * rows * cols * 4 / 1e6
     return {"pairs_per_s_e2e": round(n_batches * batch / dt, 2),
             "e2e": {"workload": f"{wl_name}, {batch} pairs per batch, {n_batches} batches "
