@@ -69,6 +69,14 @@ PATCHES = {
                 "    auto issue = [&](RowIn<G32> &d, int r) {\n"
                 "        load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(r < a ? a : (r >= b ? b - 1 : r)));\n"
                 "    };")],
+    # timing only: with the alternating directions, rows beyond the END of
+    # each stream (below b downwards, above a upwards) load the nearest
+    # segment row instead: what the end-boundary halo reads still cost
+    "haloEnd": [("    auto issue = [&](RowIn<G32> &d, int r) { load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(r)); };",
+                 "    auto issue = [&](RowIn<G32> &d, int r) {\n"
+                 "        const int rr = dir > 0 ? (r >= b ? b - 1 : r) : (r < a ? a : r);\n"
+                 "        load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(rr));\n"
+                 "    };")],
     # 4 rows of prefetch at w = 5 (the stream's loads run a row further
     # ahead; +6 VGPRs)
     "d4": [("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };",
