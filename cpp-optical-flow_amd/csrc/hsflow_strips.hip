@@ -2,8 +2,10 @@
 //
 // One wavefront owns a 128-column strip of one pair (lane l: columns 2l and
 // 2l+1 of the strip, as in K2) and a segment of N output rows of it.  It
-// streams the strip's rows top to bottom once per pass and runs the pass's
-// KB Jacobi iterations as KB time-skewed stages in registers:
+// streams the segment's rows once per pass -- even segments top to bottom,
+// odd ones bottom to top (strip_body's `dir`; written below for the
+// downward stream) -- and runs the pass's KB Jacobi iterations as KB
+// time-skewed stages in registers:
 //
 //   time step t: row t of the input state (u, v) and its packed gradients
 //     arrive (loaded D steps earlier);  stage 1 updates row t - AR to
