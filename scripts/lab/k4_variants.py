@@ -77,6 +77,19 @@ PATCHES = {
                  "        const int rr = dir > 0 ? (r >= b ? b - 1 : r) : (r < a ? a : r);\n"
                  "        load_row<X2, G32>(d, rs, ld_e, ld_o, row_off(rr));\n"
                  "    };")],
+    # progress-ranked wave priority: a wave in the first quarter of its
+    # stream runs at priority 3, the last quarter at 0, so a SIMD's lagging
+    # wave is issued first (waves that start together stay together, and
+    # the end-boundary neighbours read their shared rows closer in time)
+    "prio": [("        constexpr int FILL = decltype(fill_c)::value;\n",
+              "        constexpr int FILL = decltype(fill_c)::value;\n"
+              "        {\n"
+              "            const int q = ((tb - t_first) * dir) * 4 / nsteps;\n"
+              "            if (q <= 0) __builtin_amdgcn_s_setprio(3);\n"
+              "            else if (q == 1) __builtin_amdgcn_s_setprio(2);\n"
+              "            else if (q == 2) __builtin_amdgcn_s_setprio(1);\n"
+              "            else __builtin_amdgcn_s_setprio(0);\n"
+              "        }\n")],
     # 4 rows of prefetch at w = 5 (the stream's loads run a row further
     # ahead; +6 VGPRs)
     "d4": [("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };",
