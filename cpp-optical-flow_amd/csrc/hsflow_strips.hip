@@ -483,12 +483,19 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
         return n;
     };
     int best_n = aligned(override_rows > 0 ? override_rows : 84);
-    // w = 5 (KB 6): 84-row segments measured best on every shape that runs
-    // K4 once the pipeline fill is skipped (same box, N 48..240: 1080p x 8,
-    // 4K x 1 and x 2, and 8K, where the model below would take 168 rows and
-    // one round of waves: 1.13 M against 1.14-1.15 M Mpix*iter/s at 84,
-    // alternated on one box)
-    if (override_rows <= 0 && W == 5 && KB == 6) override_rows = best_n;
+    // w = 5 (KB 6): 84-row segments measured best on every launch that fills
+    // one round of wave slots with them (same box, N 48..240: 1080p x 8, 4K
+    // x 2, and 8K, where the model below would take 168 rows and one round
+    // of waves: 1.13 M against 1.14-1.15 M Mpix*iter/s at 84, alternated on
+    // one box).  A single pair whose 84-row waves do not fill one round
+    // takes the model's height (round 5, scripts/kernel_choice_sweep.py,
+    // profiles/r05_kernel_choice_sweep*.txt: config 5's 8K level-0 band at
+    // N = 4, 1176 rows, 48-row segments 16 % faster than 84; it keeps 84 for
+    // a 4K pair).  Batches keep 84: the model's height lost 3-30 % on 1080p
+    // x 3..7 (their halves run concurrently on the side streams)
+    if (override_rows <= 0 && W == 5 && KB == 6 &&
+        (batch > 1 || strips * ((rows + best_n - 1) / best_n) >= slots))
+        override_rows = best_n;
     if (override_rows <= 0) {
         const long simds = slots / 2 > 0 ? slots / 2 : 1;
         double best = -1.0;
@@ -517,11 +524,18 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
 // at least 0.45 of the wave slots with 84-row segments (same-box sweeps: a
 // 4K pair, 37 strips x 26 segments = 962 waves, runs K4 5 % faster than
 // K2; two 1080p pairs, 38 x 13 = 494 waves, and a single one, 247, run K2's
-// tiles 30 % faster).
+// tiles 30 % faster), or (w = 5, a single pair) at least 0.35 with 60-row
+// segments (round 5: config 5's 8K level-0 band at N = 8, 640 x 7680, 814
+// waves at 60 rows, runs K4 8 % faster than K2; a 1176 x 3840 band 16 %; a
+// 1080p pair, 342 waves, stays on K2; batches keep the 0.45 rule -- 1080p
+// x 3 on K4 lost 17 % to K2).
 bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
     int nseg = 0, nstrips = 0;
     strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 84);
-    return (long)nseg * nstrips * batch * 20 >= (long)slots * 9;  // >= 0.45 of the slots
+    if ((long)nseg * nstrips * batch * 20 >= (long)slots * 9) return true;  // >= 0.45
+    if (W != 5 || KB != 6 || batch != 1) return false;
+    strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 60);
+    return (long)nseg * nstrips * batch * 20 >= (long)slots * 7;  // >= 0.35
 }
 
 // One K4 pass of `a.batch` pairs in segments of `seg_rows` rows (the

@@ -64,7 +64,11 @@ def main():
              "4k8": (8, 2160, 3840, 120), "4k4": (4, 2160, 3840, 120),
              "1080p6": (6, 1080, 1920, 300), "1080p7": (7, 1080, 1920, 300),
              "1080p8f": (8, 1080, 1920, 300), "1080p10": (10, 1080, 1920, 300),
-             "1080p12": (12, 1080, 1920, 300), "1080p16f": (16, 1080, 1920, 300)}
+             "1080p12": (12, 1080, 1920, 300), "1080p16f": (16, 1080, 1920, 300),
+             # config 5's level-0 row bands at N = 8 / 4 / 2 (extended band,
+             # one 24-iteration chunk)
+             "band8": (1, 640, 7680, 24), "band4": (1, 1176, 7680, 24),
+             "band2": (1, 2208, 7680, 24)}
     hsflow.set_max_streams(a.streams)
     hsflow.set_iters_per_launch(a.kb)
     for name in a.cases.split(","):
