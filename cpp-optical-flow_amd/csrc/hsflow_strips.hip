@@ -491,11 +491,24 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
     // takes the model's height (round 5, scripts/kernel_choice_sweep.py,
     // profiles/r05_kernel_choice_sweep*.txt: config 5's 8K level-0 band at
     // N = 4, 1176 rows, 48-row segments 16 % faster than 84; it keeps 84 for
-    // a 4K pair).  Batches keep 84: the model's height lost 3-30 % on 1080p
-    // x 3..7 (their halves run concurrently on the side streams)
-    if (override_rows <= 0 && W == 5 && KB == 6 &&
-        (batch > 1 || strips * ((rows + best_n - 1) / best_n) >= slots))
+    // a 4K pair).  Batches do not follow the model (its heights lost 3-30 %
+    // on 1080p x 3..7, whose halves run concurrently on the side streams)
+    if (override_rows <= 0 && W == 5 && KB == 6 && batch > 1) {
+        // a batch: the tallest of 84, 72, 60, 48 rows whose waves fill 0.6 of
+        // the slots (same sweep: 1080p x 3 48 rows, 10 % faster than K2;
+        // x 4 60 rows, 11 % faster than 84; x 5..8 and 4K x 2 keep 84)
+        for (const int n : {84, 72, 60, 48}) {
+            const int na = aligned(n);
+            if (strips * ((rows + na - 1) / na) * 10 >= (long)slots * 6 || na == aligned(48)) {
+                override_rows = na;
+                break;
+            }
+        }
+        best_n = override_rows;
+    } else if (override_rows <= 0 && W == 5 && KB == 6 &&
+               strips * ((rows + best_n - 1) / best_n) >= slots) {
         override_rows = best_n;
+    }
     if (override_rows <= 0) {
         const long simds = slots / 2 > 0 ? slots / 2 : 1;
         double best = -1.0;
@@ -527,13 +540,18 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
 // tiles 30 % faster), or (w = 5, a single pair) at least 0.35 with 60-row
 // segments (round 5: config 5's 8K level-0 band at N = 8, 640 x 7680, 814
 // waves at 60 rows, runs K4 8 % faster than K2; a 1176 x 3840 band 16 %; a
-// 1080p pair, 342 waves, stays on K2; batches keep the 0.45 rule -- 1080p
-// x 3 on K4 lost 17 % to K2).
+// 1080p pair, 342 waves, stays on K2), or (w = 5, a batch) at least 0.6
+// with 48-row segments (1080p x 3: 1311 waves, K4 10 % faster than K2;
+// 1080p x 2, 874, and 720p x 4, 780, stay on K2).
 bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
     int nseg = 0, nstrips = 0;
     strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 84);
     if ((long)nseg * nstrips * batch * 20 >= (long)slots * 9) return true;  // >= 0.45
-    if (W != 5 || KB != 6 || batch != 1) return false;
+    if (W != 5 || KB != 6) return false;
+    if (batch > 1) {  // a batch whose 48-row waves fill 0.6 of the slots
+        strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 48);
+        return (long)nseg * nstrips * batch * 10 >= (long)slots * 6;
+    }
     strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 60);
     return (long)nseg * nstrips * batch * 20 >= (long)slots * 7;  // >= 0.35
 }

@@ -145,7 +145,7 @@ def size_split(mine: Sequence[int], sizes: Sequence[int]) -> List[List[int]]:
 # scripts/scale_predict.py `group_solve_ms`, profiles/r05_scale_prediction.json):
 # small batches leave most of the chip idle, so a pair costs 0.72 ms alone
 # and 0.46 ms in a batch of 8.
-GROUP_SOLVE_MS = (0.7197, 1.2483, 1.9307, 2.6395, 2.6123, 2.9441, 3.3773, 3.7075)
+GROUP_SOLVE_MS = (0.7220, 1.2672, 1.9887, 2.3102, 2.6177, 2.9458, 3.4142, 3.6790)
 # RCCL point-to-point per peer link (one xGMI link each way; an assumption
 # of a third of the link's 153 GB/s, never measured here: DESIGN.md §6)
 LINK_GBPS = 50.0
