@@ -22,32 +22,6 @@ __device__ __forceinline__ void unpack_grad(uint32_t p, float &ix, float &iy,
     it = (float)(int)__builtin_amdgcn_sbfe(p, 22, 9);
 }
 
-// The same decode for a column pair in fewer instructions (K4's per-row
-// set-up): Ix and Iy by the float-magic form, one v_bitop3 per column and
-// one packed op per pair instead of a v_bfe and a v_cvt per column.  The
-// field's sign bit is flipped (so the field reads as Ix + 1024, 0..2047)
-// and the exponent of 2^23 set in one masked xor; the float is then 2^23 +
-// Ix + 1024 exactly (Iy: its field stays at bit 11, 2^23 + (Iy + 1024) 2^11,
-// scaled back by an exact fma), and subtracting the constant leaves Ix
-// exactly.  A zero word (the buffer loads' out-of-range value) still
-// decodes to 0 in every field.  It keeps the bfe/cvt pair (its field
-// overlaps the exponent bits).
-typedef float f2v_ __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void unpack_grad_pair(uint32_t pe, uint32_t po, f2v_ &ix, f2v_ &iy,
-                                                 f2v_ &it) {
-    const f2v_ fx = {__uint_as_float((pe & 0x7FFu) ^ 0x4B000400u),
-                     __uint_as_float((po & 0x7FFu) ^ 0x4B000400u)};
-    const f2v_ fy = {__uint_as_float((pe & 0x3FF800u) ^ 0x4B200000u),
-                     __uint_as_float((po & 0x3FF800u) ^ 0x4B200000u)};
-    const f2v_ bx = {-(8388608.f + 1024.f), -(8388608.f + 1024.f)};
-    const f2v_ sy = {1.f / 2048.f, 1.f / 2048.f};
-    const f2v_ by = {-(4096.f + 1024.f), -(4096.f + 1024.f)};
-    ix = fx + bx;
-    iy = __builtin_elementwise_fma(fy, sy, by);
-    it = f2v_{(float)(int)__builtin_amdgcn_sbfe(pe, 22, 9),
-              (float)(int)__builtin_amdgcn_sbfe(po, 22, 9)};
-}
-
 // Cross-lane shifts by one lane over the whole wavefront: DPP wave_shr:1 /
 // wave_shl:1 (GFX9-family DPP, kept on gfx950).  They fuse into the consuming
 // v_add_f32 as a DPP source modifier: pure VALU, no LDS crossbar traffic.
@@ -79,6 +53,31 @@ __device__ __forceinline__ uint32_t launder_u(uint32_t x) {
 __device__ __forceinline__ float launder_f(float x) {
     asm volatile("" : "+v"(x));
     return x;
+}
+
+// The same decode for a column pair in fewer instructions (K4's per-row
+// set-up): Ix and Iy by the float-magic form, one v_bitop3 per column and
+// one packed op per pair instead of a v_bfe and a v_cvt per column.  The
+// field's sign bit is flipped (so the field reads as Ix + 1024, 0..2047)
+// and the exponent of 2^23 set in one masked xor; the float is then 2^23 +
+// Ix + 1024 exactly (Iy: its field stays at bit 11, 2^23 + (Iy + 1024) 2^11,
+// scaled back by an exact fma), and subtracting the constant leaves Ix
+// exactly.  A zero word (the buffer loads' out-of-range value) still
+// decodes to 0 in every field.  It keeps the bfe/cvt pair (its field
+// overlaps the exponent bits).
+__device__ __forceinline__ void unpack_grad_pair(uint32_t pe, uint32_t po, f2v &ix, f2v &iy,
+                                                 f2v &it) {
+    const f2v fx = {__uint_as_float((pe & 0x7FFu) ^ 0x4B000400u),
+                     __uint_as_float((po & 0x7FFu) ^ 0x4B000400u)};
+    const f2v fy = {__uint_as_float((pe & 0x3FF800u) ^ 0x4B200000u),
+                     __uint_as_float((po & 0x3FF800u) ^ 0x4B200000u)};
+    const f2v bx = {-(8388608.f + 1024.f), -(8388608.f + 1024.f)};
+    const f2v sy = {1.f / 2048.f, 1.f / 2048.f};
+    const f2v by = {-(4096.f + 1024.f), -(4096.f + 1024.f)};
+    ix = fx + bx;
+    iy = __builtin_elementwise_fma(fy, sy, by);
+    it = f2v{(float)(int)__builtin_amdgcn_sbfe(pe, 22, 9),
+              (float)(int)__builtin_amdgcn_sbfe(po, 22, 9)};
 }
 
 // Horizontal window sums of two columns per lane (e = even, o = odd column),
