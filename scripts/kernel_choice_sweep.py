@@ -24,6 +24,10 @@ SHAPES = [  # (name, batch, rows, cols)
     ("1080p4", 4, 1080, 1920), ("720p4", 4, 720, 1280), ("kitti2", 2, 375, 1242),
     ("1080p3", 3, 1080, 1920), ("1080p5", 5, 1080, 1920), ("1080p6", 6, 1080, 1920),
     ("1080p7", 7, 1080, 1920), ("1080p8", 8, 1080, 1920), ("4k2", 2, 2160, 3840),
+    # shapes no rule was fitted on (a check for regressions)
+    ("720p8", 8, 720, 1280), ("720p2", 2, 720, 1280), ("1440p2", 2, 1440, 2560),
+    ("1440p1", 1, 1440, 2560), ("4k3", 3, 2160, 3840), ("1080p12", 12, 1080, 1920),
+    ("kitti8", 8, 375, 1242), ("5k1", 1, 2880, 5120),
 ]
 
 
