@@ -538,9 +538,10 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
 // 4K pair, 37 strips x 26 segments = 962 waves, runs K4 5 % faster than
 // K2; two 1080p pairs, 38 x 13 = 494 waves, and a single one, 247, run K2's
 // tiles 30 % faster), or (w = 5, a single pair) at least 0.35 with 60-row
-// segments (round 5: config 5's 8K level-0 band at N = 8, 640 x 7680, 814
-// waves at 60 rows, runs K4 8 % faster than K2; a 1176 x 3840 band 16 %; a
-// 1080p pair, 342 waves, stays on K2), or (w = 5, a batch) at least 0.6
+// or 48-row segments (round 5: config 5's 8K level-0 band at N = 8, 640 x
+// 7680, 814 waves at 60 rows, runs K4 8 % faster than K2; a 1176 x 3840
+// band 16 %; a 1440p pair, 750 waves at 48 rows, 12 %; a 1080p pair, 437
+// at 48, stays on K2), or (w = 5, a batch) at least 0.6
 // with 48-row segments (1080p x 3: 1311 waves, K4 10 % faster than K2;
 // 1080p x 2, 874, and 720p x 4, 780, stay on K2).
 bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
@@ -552,8 +553,11 @@ bool strip_fills(int W, int KB, int rows, int cols, int batch, int slots) {
         strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 48);
         return (long)nseg * nstrips * batch * 10 >= (long)slots * 6;
     }
-    strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, 60);
-    return (long)nseg * nstrips * batch * 20 >= (long)slots * 7;  // >= 0.35
+    for (const int n : {60, 48}) {  // a single pair: >= 0.35 at 60 or 48 rows
+        strip_seg_rows(W, KB, rows, cols, batch, slots, &nseg, &nstrips, n);
+        if ((long)nseg * nstrips * batch * 20 >= (long)slots * 7) return true;
+    }
+    return false;
 }
 
 // One K4 pass of `a.batch` pairs in segments of `seg_rows` rows (the
