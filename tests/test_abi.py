@@ -244,3 +244,32 @@ void snippet(void) {
                               "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
                              capture_output=True, text=True)
         assert out.returncode == 0, f"INTEGRATION.md C snippet {k}:\n{b}\n{out.stderr}"
+
+
+def test_kernel_choice_rules_for_partial_fills():
+    """The round-5 kernel choice for launches that fill part of the chip
+    (w = 5; scripts/kernel_choice_sweep.py measured each case on the GPU,
+    profiles/r05_kernel_choice_sweep*.txt): a single pair takes K4 when
+    60- or 48-row segments fill 0.35 of the wave slots, a batch when 48-row
+    segments fill 0.6; everything else keeps the 84-row rule.  The choice
+    is host logic (no GPU call; without a device the library assumes
+    MI355X's 256 CUs)."""
+    strip, tiles = "hs_jacobi_strip_kernel", "hs_jacobi_wg_kernel"
+    cases = {
+        (640, 7680, 1): strip,    # config 5's 8K level-0 band at N = 8 (K4 +8 %)
+        (1176, 7680, 1): strip,   # ... at N = 4
+        (1176, 3840, 1): strip,   # a 4K-level band at N = 2 (K4 +16 %)
+        (1440, 2560, 1): strip,   # a 1440p pair (K4 +9 %)
+        (464, 3840, 1): tiles,    # small bands stay on K2 (K2 fastest there)
+        (732, 3840, 1): tiles,
+        (1080, 1920, 1): tiles,   # the reference's single 1080p pair
+        (1080, 1920, 2): tiles,
+        (1080, 1920, 3): strip,   # K4 at 48 rows, +11 % over K2
+        (1080, 1920, 8): strip,   # the headline batch
+        (720, 1280, 4): tiles,
+        (375, 1242, 8): tiles,
+        (2160, 3840, 1): strip,
+        (2160, 3840, 2): strip,
+    }
+    for (rows, cols, batch), name in cases.items():
+        assert hsflow.jacobi_kernel_name(rows, cols, batch, 5) == name, (rows, cols, batch)
