@@ -755,6 +755,10 @@ int hsflow_set_max_streams(int n) {
 
 int hsflow_max_streams(void) { return g_split_override; }
 
+int hsflow_set_output_hugepages(int on) {
+    return hsflow::g_output_hugepages.exchange(on ? 1 : 0);
+}
+
 int hsflow_iters_per_launch(int rows, int cols, int batch, int window) {
     if (window < 1 || window > HSFLOW_MAX_WINDOW) return HSFLOW_ERR_ARG;
     if (!sizes_ok(rows, cols, batch)) return HSFLOW_ERR_ARG;

@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <vector>
 
 namespace hsflow {
@@ -60,6 +61,8 @@ bool fill_limited(int W, int KB, bool strip, int rows, int cols, int batch, int 
 // ---- host I/O of the host-buffer entry points (hsflow_hostio.cpp) ----
 // threads of the host copy pool (the caller included)
 int host_pool_width();
+// hsflow_set_output_hugepages: advise MADV_HUGEPAGE on f64 outputs (1, default)
+extern std::atomic<int> g_output_hugepages;
 // n dense device f32 planes -> host rows (f64 when `f64`, else f32; row step
 // `step`).  f32: DMA copies straight into the rows.  f64: through `stage`
 // (n * rows * cols floats, pinned) in row chunks, each widened by the pool

@@ -271,7 +271,6 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
     recv_groups: List[Tuple[torch.Tensor, torch.Tensor, list]] = []
     if rank == 0:
         scatter_reqs = []
-        _fence([stream[0][0]] if stream else [])
         for c in range(n_groups):
             ops = []
             for dst in range(1, world):
@@ -282,6 +281,10 @@ def run_stream_pipelined(stream: Optional[Sequence[Pair]], n_pairs: int, shape, 
                     ops.append(dist.P2POp(dist.isend, I0.to(device).contiguous(), dst))
                     ops.append(dist.P2POp(dist.isend, I1.to(device).contiguous(), dst))
             if ops:
+                # fenced after the send tensors exist: a .to() / .contiguous()
+                # that really copies is queued before gloo reads the buffer
+                # (as scatter_pairs does)
+                _fence([op.tensor for op in ops])
                 scatter_reqs.extend(dist.batch_isend_irecv(ops))
     else:
         for grp in groups[rank]:

@@ -52,10 +52,9 @@ EXPORTS = (
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
     "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
     "hsflow_download_device", "hsflow_jacobi_kernel_name", "hsflow_set_strip_rows",
-    "hsflow_max_streams",
+    "hsflow_max_streams", "hsflow_set_output_hugepages",
     "hsflow_flow_multi_release",
 )
-BUILD_PROBE = 1  # hsflow_build_flags(): the diagnostic (env-honouring) build
 
 
 class HsflowError(RuntimeError):
@@ -113,6 +112,8 @@ def lib():
     L.hsflow_set_iters_per_launch.argtypes = [i]
     L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
     L.hsflow_set_max_streams.argtypes = [i]
+    L.hsflow_set_output_hugepages.argtypes = [i]
+    L.hsflow_set_output_hugepages.restype = i
     L.hsflow_max_streams.argtypes = []
     L.hsflow_set_jacobi_kernel.argtypes = [i]
     L.hsflow_set_strip_rows.argtypes = [i]
@@ -443,7 +444,15 @@ def build_flags() -> int:
 
 
 def is_probe_build() -> bool:
-    return bool(build_flags() & BUILD_PROBE)
+    """True for a non-product build (hsflow_build_flags() != 0)."""
+    return build_flags() != 0
+
+
+def set_output_hugepages(on: bool) -> bool:
+    """hsflow_set_output_hugepages: MADV_HUGEPAGE advice on f64 host outputs
+    (default on; the advice stays on the caller's allocation).  Returns the
+    previous setting."""
+    return bool(lib().hsflow_set_output_hugepages(1 if on else 0))
 
 
 def workspace_bytes(rows: int, cols: int, batch: int = 1) -> int:

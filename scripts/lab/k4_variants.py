@@ -19,7 +19,7 @@ Variants (timing questions about K4's issue limit):
   haloL2    halo rows read as the nearest segment row (timing only): the
             cost of the segments' halo re-reads
   d4        4 rows of prefetch instead of 3 at w = 5
-`probe` runs 1080p x 8 and 4K x 2 solves (hipGraph replays after a 0.15 s
+`probe` runs 1080p x 8 and 4K x 2 solves (K4_SHAPES=4k1,1080p1,...: other shapes) (hipGraph replays after a 0.15 s
 pre-warm) with each build in its own process, alternating the order twice,
 and prints Mpix*iter/s per build."""
 import json
@@ -95,6 +95,33 @@ PATCHES = {
     "d4": [("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };",
             "template <> struct StripCfg<5, 6> { static constexpr int D = 4, U = 12; };")],
     # a barrier every second step only
+    # launch bounds of one wave per SIMD (the single-pair launches run ~1
+    # wave per SIMD anyway): the allocator may use 512 registers
+    "lb1": [("__launch_bounds__(64, 2) void hs_jacobi_strip_kernel",
+             "__launch_bounds__(64, 1) void hs_jacobi_strip_kernel")],
+    "d4lb1": [("__launch_bounds__(64, 2) void hs_jacobi_strip_kernel",
+               "__launch_bounds__(64, 1) void hs_jacobi_strip_kernel"),
+              ("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };",
+               "template <> struct StripCfg<5, 6> { static constexpr int D = 4, U = 12; };")],
+    "d6lb1": [("__launch_bounds__(64, 2) void hs_jacobi_strip_kernel",
+               "__launch_bounds__(64, 1) void hs_jacobi_strip_kernel"),
+              ("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };",
+               "template <> struct StripCfg<5, 6> { static constexpr int D = 6, U = 12; };")],
+    # timing only (wrong values): the stage chain of a time step cut in two
+    # -- stages KB/2.. take the level-(KB/2) sums of the PREVIOUS step -- so
+    # a lone wave has two independent dependency chains per step: is the
+    # single-pair launch latency-bound on the serial stage chain?
+    "split": [('    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n', "    f2v chu = {0.f, 0.f}, chv = {0.f, 0.f};\n" + '    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n'),
+              ('                if (kf < 2 * AR * j) break;  // nor any later stage\n', '                if (kf < 2 * AR * j) break;  // nor any later stage\n' + "                if (j == KB / 2) { const f2v a0 = hu, a1 = hv; hu = chu; hv = chv; chu = a0; chv = a1; }\n")],
+    "split3": [('    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n', "    f2v chu = {0.f, 0.f}, chv = {0.f, 0.f}, dhu = {0.f, 0.f}, dhv = {0.f, 0.f};\n" + '    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n'),
+               ('                if (kf < 2 * AR * j) break;  // nor any later stage\n', '                if (kf < 2 * AR * j) break;  // nor any later stage\n' + "                if (j == 2) { const f2v a0 = hu, a1 = hv; hu = chu; hv = chv; chu = a0; chv = a1; }\n"
+                         "                if (j == 4) { const f2v a0 = hu, a1 = hv; hu = dhu; hv = dhv; dhu = a0; dhv = a1; }\n")],
+    # timing only: no memory traffic (every load / store out of range, the
+    # same instructions), loads only out of range, stores only
+    "nomem": [('        return (unsigned)r < (unsigned)rows ? r * row_bytes : (int)0x80000000;', "        return (int)0x80000000; (void)r;"),
+              ('                    const int so = sin ? y * row_bytes : (int)0x80000000;', "                    const int so = (int)0x80000000; (void)sin;")],
+    "noload": [('        return (unsigned)r < (unsigned)rows ? r * row_bytes : (int)0x80000000;', "        return (int)0x80000000; (void)r;")],
+    "nostore": [('                    const int so = sin ? y * row_bytes : (int)0x80000000;', "                    const int so = (int)0x80000000; (void)sin;")],
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
 }
@@ -129,7 +156,10 @@ import hsflow
 hsflow.LIB_PATH = %(lib)r
 import numpy as np, torch
 out = {}
-for tag, batch, rows, cols, iters in (("1080p8", 8, 1080, 1920, 300), ("4k2", 2, 2160, 3840, 500)):
+SHAPES = {"1080p8": (8, 1080, 1920, 300), "4k2": (2, 2160, 3840, 500),
+          "4k1": (1, 2160, 3840, 500), "1080p1": (1, 1080, 1920, 300)}
+for tag in os.environ.get("K4_SHAPES", "1080p8,4k2").split(","):
+    batch, rows, cols, iters = SHAPES[tag]
     ps = [hsflow.synth_pair(1000 + i, rows, cols) for i in range(batch)]
     I0 = torch.from_numpy(np.stack([p[0] for p in ps])).cuda()
     I1 = torch.from_numpy(np.stack([p[1] for p in ps])).cuda()

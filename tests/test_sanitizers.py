@@ -79,3 +79,23 @@ def test_host_copy_pool_under_tsan(tmp_path):
     r = subprocess.run([exe, "6", "400"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
     assert "0 wrong items" in r.stdout
+
+
+def test_f64_widening_under_tsan(tmp_path):
+    """The host half of an f64 download (hsflow_widen.h): the page pre-touch
+    (one zero byte per page of the output rows) and the widening of the
+    same rows never overlap (they once ran as one pool job whose
+    items finish out of order), no data race under ThreadSanitizer, and
+    every widened value survives."""
+    if subprocess.run(["g++", "--version"], capture_output=True).returncode != 0:
+        pytest.skip("no g++")
+    exe = str(tmp_path / "widen_tsan")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+                           "-DHSFLOW_PLAIN_WIDEN",
+                           "-I", os.path.join(ROOT, "cpp-optical-flow_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "cpp", "widen_tsan.cpp"), "-o", exe])
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([exe, "30"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
+    assert "0 wrong values" in r.stdout
