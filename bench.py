@@ -889,9 +889,15 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
     # groups keep the exposed return of the last (u, v) short;
     # frame_parallel.run_stream_pipelined, scripts/scale_predict.py)
     in_mb, out_mb = 2 * rows * cols / 1e6, 2 * rows * cols * 4 / 1e6
+    # the model's link rate measured on this node's links before the timed
+    # passes (one f32 plane per round trip, rank 0 to each peer; the slowest
+    # peer's rate, broadcast so every rank picks the same groups), in place
+    # of the assumed frame_parallel.LINK_GBPS
+    link = fp.measure_link_gbps(dev, rank, world, rows * cols * 4) if world > 1 else None
+    link_gbps = link["link_gbps"] if link else fp.LINK_GBPS
 
     def sizes(share):
-        return fp.group_sizes(share, world, in_mb, out_mb)
+        return fp.group_sizes(share, world, in_mb, out_mb, link_gbps=link_gbps)
 
     my_sizes = sizes(len(mine))
     if solve_batch is None:
@@ -925,6 +931,9 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
     leg = {"pairs_per_s": round(n * steps / elapsed, 2),
            "ms_per_pass": round(elapsed / steps * 1e3, 3), "pairs": n,
            "groups_per_rank": len(my_sizes), "group_sizes": my_sizes,
+           "link_gbps_measured": (round(link["link_gbps"], 2) if link else None),
+           "link_gbps_per_peer": (link["per_peer"] if link and rank == 0 else None),
+           "link_gbps_model": round(link_gbps, 2),
            "frames": "u8",
            "Mpix_iter_per_s": round(n * steps * rows * cols * iters / elapsed / 1e6, 1),
            "transport": _transport(world, dev),

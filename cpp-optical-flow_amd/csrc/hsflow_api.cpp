@@ -747,6 +747,19 @@ const char *hsflow_jacobi_kernel_name(int rows, int cols, int batch, int window)
     return window >= 3 ? "hs_jacobi_wg_kernel" : "hs_jacobi_kernel";
 }
 
+int hsflow_strip_seg_rows(int rows, int cols, int batch, int window) {
+    if (window < 1 || window > HSFLOW_MAX_WINDOW || !sizes_ok(rows, cols, batch)) return 0;
+    if (!plan_passes(window, true, rows, cols, batch).strip) return 0;
+    if (g_strip_rows > 0) {
+        int nseg = 0, nstrips = 0;
+        return hsflow::strip_seg_rows(window, strip_kb(window), rows, cols, batch, 1, &nseg,
+                                      &nstrips, g_strip_rows);
+    }
+    int nseg = 0, nstrips = 0;
+    return hsflow::strip_seg_rows(window, strip_kb(window), rows, cols, batch,
+                                  8 * hsflow::device_cus(), &nseg, &nstrips, 0);
+}
+
 int hsflow_set_max_streams(int n) {
     if (n < 0 || n > 16) return HSFLOW_ERR_ARG;
     g_split_override = n;

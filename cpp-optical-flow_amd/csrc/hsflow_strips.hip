@@ -295,16 +295,28 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // update of the next 2 AR steps, whose rows are not needed either, gave
     // 1-ulp differences in a segment's first rows on the GPU, not kept.)
     static_assert(2 * AR * KB == 2 * U, "the pipeline fill is two blocks");
-    auto block = [&](int tb, auto rowe_c, auto fill_c) {
+    // PLAIN: every row the block loads lies inside the image and every row
+    // it stores inside the segment, so the offsets are the rows' own (one
+    // scalar add per row from the block's base, no compare / select: the
+    // interior blocks of every stream; round 6, a single 4K pair's lone
+    // waves issue every instruction, SALU included)
+    const int drb = dir * row_bytes;
+    auto block = [&](int tb, auto rowe_c, auto fill_c, auto plain_c) {
         constexpr bool ROWE = decltype(rowe_c)::value;
         constexpr int FILL = decltype(fill_c)::value;
+        constexpr bool PLAIN = decltype(plain_c)::value;
+        // byte offset of the block's first stage-KB row (PLAIN blocks)
+        const int ob = PLAIN ? (tb - dir * (KB * AR)) * row_bytes : 0;
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const int t = tb + dir * k;
             // 1. this row's input (loaded D steps ago), then the load of
             //    the row D steps ahead into the freed slot
             const RowIn<G32> cur = buf[k % D];
-            issue(buf[k % D], t + dir * D);
+            if constexpr (PLAIN)
+                load_row<X2, G32>(buf[k % D], rs, ld_e, ld_o, ob + (k + KB * AR + D) * drb);
+            else
+                issue(buf[k % D], t + dir * D);
             // 2. level-0 horizontal sums of row t
             f2v hu, hv;
             hrow<W>(cur.u, cur.v, hu, hv);
@@ -344,7 +356,8 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                     // counts them in its vmcnt waits, which keep the loads
                     // of the D rows ahead in flight
                     const bool sin = y >= a && y < b;
-                    const int so = sin ? y * row_bytes : (int)0x80000000;
+                    const int so =
+                        PLAIN ? ob + k * drb : (sin ? y * row_bytes : (int)0x80000000);
                     const int oe = st_e;
                     // nt, or write-through (sc1) in launches that leave most
                     // of the chip idle (WT, from p.write_through: a 4K pair
@@ -392,17 +405,30 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
         const int hi = dir > 0 ? e - AR : tb + KB * AR;
         return lo >= 0 && hi < rows;
     };
+    // ... and PLAIN (above): its loads D rows ahead inside the image, its
+    // stage-KB rows inside [a, b) (false only near the stream's ends)
+    auto within = [&](int r0, int r1, int lo, int hi) {
+        return (r0 < r1 ? r0 : r1) >= lo && (r0 < r1 ? r1 : r0) < hi;
+    };
+    auto plain = [&](int tb) {
+        const int e = tb + dir * (U - 1);
+        return inside(tb) && within(tb + dir * D, e + dir * D, 0, rows) &&
+               within(tb - dir * (KB * AR), e - dir * (KB * AR), a, b);
+    };
     const int nblk = (nsteps + U - 1) / U;
     int tb = t_first, ib = 2;
-    block(tb, std::true_type{}, std::integral_constant<int, 1>{});
+    using NP = std::false_type;
+    block(tb, std::true_type{}, std::integral_constant<int, 1>{}, NP{});
     tb += dir * U;
-    block(tb, std::true_type{}, std::integral_constant<int, 2>{});
+    block(tb, std::true_type{}, std::integral_constant<int, 2>{}, NP{});
     tb += dir * U;
     if constexpr (X2 && !G32) {
-        for (; ib < nblk && !inside(tb); tb += dir * U, ++ib) block(tb, std::true_type{}, F0{});
-        for (; ib < nblk && inside(tb); tb += dir * U, ++ib) block(tb, std::false_type{}, F0{});
+        for (; ib < nblk && !inside(tb); tb += dir * U, ++ib)
+            block(tb, std::true_type{}, F0{}, NP{});
+        for (; ib < nblk && plain(tb); tb += dir * U, ++ib)
+            block(tb, std::false_type{}, F0{}, std::true_type{});
     }
-    for (; ib < nblk; tb += dir * U, ++ib) block(tb, std::true_type{}, F0{});
+    for (; ib < nblk; tb += dir * U, ++ib) block(tb, std::true_type{}, F0{}, NP{});
 }
 
 // ---------------------------------------------------------------- kernel
@@ -411,8 +437,8 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
 // (strips fastest), so the strips that share halo columns run side by side;
 // the XCD-aware remap gives each XCD a contiguous run of them (its L2
 // serves the shared halo columns and the rows two segments both read).
-template <int W, int KB, int D, int U, bool WT>
-__global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs p) {
+template <int W, int KB, int D, int U, int WPE, bool WT>
+__global__ __launch_bounds__(64, WPE) void hs_jacobi_strip_kernel(const JacobiArgs p) {
     const int nblk = gridDim.x;
     const int lin = blockIdx.x;
     const int qn = nblk >> 3, rem = nblk & 7, xcd = lin & 7;
@@ -452,12 +478,32 @@ __global__ __launch_bounds__(64, 2) void hs_jacobi_strip_kernel(const JacobiArgs
 
 // ------------------------------------------------------------- launcher
 namespace {
+// D rows of prefetch, U = KB AR steps per unrolled block, WPE waves per SIMD
+// the register budget is sized for (w = 5, KB 4: 3 waves, <= 168 VGPRs)
 template <int W, int KB> struct StripCfg;
-template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12; };
-template <> struct StripCfg<3, 8> { static constexpr int D = 2, U = 8; };
+template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12, WPE = 2; };
+template <> struct StripCfg<5, 5> { static constexpr int D = 5, U = 10, WPE = 2; };
+template <> struct StripCfg<5, 4> { static constexpr int D = 2, U = 8, WPE = 3; };
+template <> struct StripCfg<3, 8> { static constexpr int D = 2, U = 8, WPE = 2; };
+
+template <int W, int KB>
+void launch_cfg(const JacobiArgs &a, dim3 grd, bool wt, hipStream_t s) {
+    using C = StripCfg<W, KB>;
+    if (wt)
+        hipLaunchKernelGGL((hs_jacobi_strip_kernel<W, KB, C::D, C::U, C::WPE, true>), grd,
+                           dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((hs_jacobi_strip_kernel<W, KB, C::D, C::U, C::WPE, false>), grd,
+                           dim3(64), 0, s, a);
+}
 }  // namespace
 
-bool strip_supported(int W, int KB) { return (W == 5 && KB == 6) || (W == 3 && KB == 8); }
+// w = 5 at KB 6 (the default depth) and the shallower 5 and 4 (fewer
+// registers per wave: more waves per SIMD for launches that fill part of
+// the chip), w = 3 at KB 8
+bool strip_supported(int W, int KB) {
+    return (W == 5 && KB >= 4 && KB <= 6) || (W == 3 && KB == 8);
+}
 
 // Segment rows for a launch.  Each wave streams N rows plus the KB (W - 1)
 // halo rows its stages need: tall segments waste little work and re-read
@@ -466,15 +512,15 @@ bool strip_supported(int W, int KB) { return (W == 5 && KB == 6) || (W == 3 && K
 // streamed row, two waves sharing a SIMD ~0.75 us each; a launch's waves
 // come in rounds of 2 per SIMD (the last round at 1 per SIMD if it has at
 // most one wave per SIMD); the pass cannot beat its row loads (1.5 KB per
-// wave-row) at ~5 TB/s.  Candidates: N >= 48 with N + KB (W - 1) a
-// multiple of the unroll period, up to 240 rows.  `override_rows` > 0
+// wave-row) at ~5 TB/s.  Candidates: N >= 48 (w = 5: N >= 12) with N + KB
+// (W - 1) a multiple of the unroll period, up to 240 rows.  `override_rows` > 0
 // forces N (rounded up to the period).
 int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int *nseg_out,
                    int *nstrips_out, int override_rows) {
     const int A = W - W / 2 - 1, AR = W / 2;
     const int HLc = KB * A + ((KB * A) & 1), HRc = KB * AR + ((KB * AR) & 1);
     const int ox = 128 - HLc - HRc;
-    const int U = (W == 5) ? 12 : 8;
+    const int U = KB * AR;  // the unroll period (StripCfg)
     const int nstrips = (cols + ox - 1) / ox;
     const long strips = (long)nstrips * batch;
     const int halo = KB * (W - 1);
@@ -512,8 +558,13 @@ int strip_seg_rows(int W, int KB, int rows, int cols, int batch, int slots, int 
     if (override_rows <= 0) {
         const long simds = slots / 2 > 0 ? slots / 2 : 1;
         double best = -1.0;
-        for (int n = aligned(48); n <= 240; n = aligned(n + 1)) {
+        // w = 5 also below 48 rows while every wave runs alone on its SIMD
+        // (round 6: a 1440p pair at 36 rows, 1000 waves, 15 % faster than
+        // at 48 -- profiles/r06_kb_sweep.txt); others from 48
+        const int n0 = (W == 5 && KB == 6) ? 12 : 48;
+        for (int n = aligned(n0); n <= 240; n = aligned(n + 1)) {
             const long w = strips * ((rows + n - 1) / n);
+            if (n < 48 && w > simds) continue;
             const long rounds = (w + slots - 1) / slots;
             const long last = w - (rounds - 1) * slots;
             const int steps = n + halo;
@@ -572,25 +623,16 @@ hipError_t launch_jacobi_strip(JacobiArgs a, int W, int KB, int seg_rows, hipStr
     if (waves <= 0 || waves > 0x7FFFFFFFL) return hipErrorInvalidValue;
     dim3 grd((unsigned)waves, 1, 1);
     const bool wt = a.write_through != 0;
-    if (W == 5 && KB == 6) {
-        using C = StripCfg<5, 6>;
-        if (wt)
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U, true>), grd, dim3(64), 0,
-                               s, a);
-        else
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<5, 6, C::D, C::U, false>), grd, dim3(64), 0,
-                               s, a);
-    } else if (W == 3 && KB == 8) {
-        using C = StripCfg<3, 8>;
-        if (wt)
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U, true>), grd, dim3(64), 0,
-                               s, a);
-        else
-            hipLaunchKernelGGL((hs_jacobi_strip_kernel<3, 8, C::D, C::U, false>), grd, dim3(64), 0,
-                               s, a);
-    } else {
+    if (W == 5 && KB == 6)
+        launch_cfg<5, 6>(a, grd, wt, s);
+    else if (W == 5 && KB == 5)
+        launch_cfg<5, 5>(a, grd, wt, s);
+    else if (W == 5 && KB == 4)
+        launch_cfg<5, 4>(a, grd, wt, s);
+    else if (W == 3 && KB == 8)
+        launch_cfg<3, 8>(a, grd, wt, s);
+    else
         return hipErrorInvalidValue;
-    }
     return hipGetLastError();
 }
 

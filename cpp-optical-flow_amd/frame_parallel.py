@@ -147,8 +147,58 @@ def size_split(mine: Sequence[int], sizes: Sequence[int]) -> List[List[int]]:
 # and 0.46 ms in a batch of 8.
 GROUP_SOLVE_MS = (0.7220, 1.2672, 1.9887, 2.3102, 2.6177, 2.9458, 3.4142, 3.6790)
 # RCCL point-to-point per peer link (one xGMI link each way; an assumption
-# of a third of the link's 153 GB/s, never measured here: DESIGN.md §6)
+# of a third of the link's 153 GB/s: DESIGN.md §6).  Only the fallback: the
+# stream leg measures the link before its timed passes (measure_link_gbps)
+# and sizes its groups with that rate.
 LINK_GBPS = 50.0
+
+
+def measure_link_gbps(device, rank: int, world: int, nbytes: int, reps: int = 3) -> dict:
+    """The point-to-point rate of rank 0's link to every peer, measured with
+    the transport the stream uses: per peer, `reps` round trips of one
+    `nbytes` buffer (0 -> peer -> 0; the peers take turns, the others idle),
+    rate = nbytes / (best round trip / 2).  Rank 0 broadcasts the result, so
+    every rank sizes its groups (group_sizes) with the same value: the
+    slowest peer's rate (`link_gbps`), or LINK_GBPS if a measurement is not
+    finite and positive.  Returns {"link_gbps", "per_peer"} on every rank.
+    Runs outside any timed region; one call costs ~2 reps (world - 1)
+    transfers of nbytes (7 peers x 3 x 2 x 8.3 MB at 50 GB/s: ~7 ms)."""
+    import time
+    per_peer: List[float] = []
+    if world > 1:
+        buf = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=device)
+        buf.fill_(1.0)
+        sync = ((lambda: torch.cuda.synchronize(device)) if buf.is_cuda else (lambda: None))
+        for peer in range(1, world):
+            best = float("inf")
+            for it in range(reps + 1):  # the first round trip warms the path
+                dist.barrier()
+                if rank == 0:
+                    sync()
+                    t0 = time.perf_counter()
+                    _fence([buf])
+                    dist.send(buf, peer)
+                    dist.recv(buf, peer)
+                    sync()
+                    if it > 0:
+                        best = min(best, time.perf_counter() - t0)
+                elif rank == peer:
+                    dist.recv(buf, 0)
+                    sync()
+                    dist.send(buf, 0)
+                    sync()
+            if rank == 0:
+                per_peer.append(buf.numel() * 4 / (best / 2) / 1e9 if best > 0 else 0.0)
+        val = torch.tensor([min(per_peer) if per_peer else LINK_GBPS], dtype=torch.float64)
+        if dist.get_backend() == "nccl":
+            val = val.to(device)
+        dist.broadcast(val, 0)
+        rate = float(val.item())
+    else:
+        rate = LINK_GBPS
+    if not (rate > 0.0 and rate < float("inf")):
+        rate = LINK_GBPS
+    return {"link_gbps": rate, "per_peer": [round(x, 2) for x in per_peer]}
 
 
 def pipeline_ms(sizes: Sequence[int], in_mb: float, out_mb: float,

@@ -52,7 +52,7 @@ EXPORTS = (
     "hsflow_flow_bgr", "hsflow_pyramid_build_device", "hsflow_upflow_device",
     "hsflow_set_jacobi_kernel", "hsflow_build_flags", "hsflow_flow_multi",
     "hsflow_download_device", "hsflow_jacobi_kernel_name", "hsflow_set_strip_rows",
-    "hsflow_max_streams", "hsflow_set_output_hugepages",
+    "hsflow_max_streams", "hsflow_set_output_hugepages", "hsflow_strip_seg_rows",
     "hsflow_flow_multi_release",
 )
 
@@ -112,6 +112,8 @@ def lib():
     L.hsflow_set_iters_per_launch.argtypes = [i]
     L.hsflow_iters_per_launch.argtypes = [i, i, i, i]
     L.hsflow_set_max_streams.argtypes = [i]
+    L.hsflow_strip_seg_rows.argtypes = [i, i, i, i]
+    L.hsflow_strip_seg_rows.restype = i
     L.hsflow_set_output_hugepages.argtypes = [i]
     L.hsflow_set_output_hugepages.restype = i
     L.hsflow_max_streams.argtypes = []
@@ -446,6 +448,12 @@ def build_flags() -> int:
 def is_probe_build() -> bool:
     """True for a non-product build (hsflow_build_flags() != 0)."""
     return build_flags() != 0
+
+
+def strip_seg_rows(rows: int, cols: int, batch: int = 1, window: int = 5) -> int:
+    """hsflow_strip_seg_rows: K4 segment height a solve of this shape uses
+    (0 when its full-depth passes run another kernel)."""
+    return int(lib().hsflow_strip_seg_rows(rows, cols, batch, window))
 
 
 def set_output_hugepages(on: bool) -> bool:

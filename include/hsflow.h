@@ -172,6 +172,11 @@ int hsflow_set_strip_rows(int seg_rows);
  * a static string.  For profiles and the bench's roofline record. */
 const char *hsflow_jacobi_kernel_name(int rows, int cols, int batch, int window);
 
+/* Rows per K4 segment that a solve of this shape uses under the current
+ * settings (hsflow_set_strip_rows, else the automatic choice); 0 when its
+ * full-depth passes do not run K4.  For profiles and tests. */
+int hsflow_strip_seg_rows(int rows, int cols, int batch, int window);
+
 /* Batches of >= 2 pairs are split over side streams (forked from and joined
  * back to the caller's stream with events) so that concurrent Jacobi
  * launches overlap.  0 = automatic (default): 2 streams for eager calls, no

@@ -3,7 +3,8 @@ fill part of the chip (single pairs, small batches, config 5's row bands)?
 Graph-replayed jacobi_device passes only (gradients once, outside the
 timing), 48 iterations (8 passes), after a 0.15 s pre-warm; K2 against K4
 at several segment heights, per shape.  Prints one JSON line per shape.
-    python scripts/kernel_choice_sweep.py [--rows-list 36,48,60,72,84]"""
+    python scripts/kernel_choice_sweep.py [--rows-list 36,48,60,72,84]
+        [--kb-list 4,5 --iters 120]   # also K4 at other depths"""
 import argparse
 import json
 import os
@@ -31,9 +32,10 @@ SHAPES = [  # (name, batch, rows, cols)
 ]
 
 
-def timed_passes(rows, cols, batch, iters, kernel, seg_rows, ws, u, v):
+def timed_passes(rows, cols, batch, iters, kernel, seg_rows, ws, u, v, kb=0):
     hsflow.set_jacobi_kernel(kernel)
     hsflow.set_strip_rows(seg_rows)
+    hsflow.set_iters_per_launch(kb)
     try:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -62,6 +64,7 @@ def timed_passes(rows, cols, batch, iters, kernel, seg_rows, ws, u, v):
     finally:
         hsflow.set_jacobi_kernel(0)
         hsflow.set_strip_rows(0)
+        hsflow.set_iters_per_launch(0)
 
 
 def main():
@@ -69,6 +72,9 @@ def main():
     ap.add_argument("--rows-list", default="36,48,60,72,84")
     ap.add_argument("--iters", type=int, default=48)
     ap.add_argument("--shapes", default="")
+    # K4 depths to sweep besides the default (round 6: w = 5 K4 is built at
+    # KB 4, 5 and 6; use --iters divisible by each, e.g. 120)
+    ap.add_argument("--kb-list", default="")
     a = ap.parse_args()
     want = set(a.shapes.split(",")) if a.shapes else None
     for name, batch, rows, cols in SHAPES:
@@ -89,6 +95,10 @@ def main():
         rec["k2_ms"] = round(timed_passes(rows, cols, batch, a.iters, 2, 0, ws, u, v), 4)
         for n in [int(x) for x in a.rows_list.split(",")]:
             rec[f"k4_{n}_ms"] = round(timed_passes(rows, cols, batch, a.iters, 4, n, ws, u, v), 4)
+        for kb in [int(x) for x in a.kb_list.split(",") if x]:
+            for n in [int(x) for x in a.rows_list.split(",")]:
+                rec[f"k4kb{kb}_{n}_ms"] = round(
+                    timed_passes(rows, cols, batch, a.iters, 4, n, ws, u, v, kb=kb), 4)
         best = min((k for k in rec if k.endswith("_ms")), key=lambda k: rec[k])
         rec["best"] = best
         rec["auto_over_best"] = round(rec["auto_ms"] / rec[best], 3)

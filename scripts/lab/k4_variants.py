@@ -122,6 +122,12 @@ PATCHES = {
               ('                    const int so = sin ? y * row_bytes : (int)0x80000000;', "                    const int so = (int)0x80000000; (void)sin;")],
     "noload": [('        return (unsigned)r < (unsigned)rows ? r * row_bytes : (int)0x80000000;', "        return (int)0x80000000; (void)r;")],
     "nostore": [('                    const int so = sin ? y * row_bytes : (int)0x80000000;', "                    const int so = (int)0x80000000; (void)sin;")],
+    # issue cost of one more instruction per time step, by type (timing
+    # calibration of a lone wave): 16 independent v_mov, 16 v_pk_add_f32,
+    # 16 s_mov per step, results unused
+    "valu16": [('            __builtin_amdgcn_sched_barrier(0);\n', '            { int d0_, d1_, d2_, d3_; asm volatile("v_mov_b32 %0, 0\\nv_mov_b32 %1, 1\\nv_mov_b32 %2, 2\\nv_mov_b32 %3, 3\\nv_mov_b32 %0, 4\\nv_mov_b32 %1, 5\\nv_mov_b32 %2, 6\\nv_mov_b32 %3, 7\\nv_mov_b32 %0, 8\\nv_mov_b32 %1, 9\\nv_mov_b32 %2, 10\\nv_mov_b32 %3, 11\\nv_mov_b32 %0, 12\\nv_mov_b32 %1, 13\\nv_mov_b32 %2, 14\\nv_mov_b32 %3, 15" : "=v"(d0_), "=v"(d1_), "=v"(d2_), "=v"(d3_)); }\n            __builtin_amdgcn_sched_barrier(0);\n')],
+    "pk16": [('            __builtin_amdgcn_sched_barrier(0);\n', '            { f2v d0_, d1_, d2_, d3_; asm volatile("v_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4\\nv_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4\\nv_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4\\nv_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4" : "=v"(d0_), "=v"(d1_), "=v"(d2_), "=v"(d3_) : "v"(colm)); }\n            __builtin_amdgcn_sched_barrier(0);\n')],
+    "salu16": [('            __builtin_amdgcn_sched_barrier(0);\n', '            { int d0_, d1_, d2_, d3_; asm volatile("s_mov_b32 %0, 0\\ns_mov_b32 %1, 1\\ns_mov_b32 %2, 2\\ns_mov_b32 %3, 3\\ns_mov_b32 %0, 4\\ns_mov_b32 %1, 5\\ns_mov_b32 %2, 6\\ns_mov_b32 %3, 7\\ns_mov_b32 %0, 8\\ns_mov_b32 %1, 9\\ns_mov_b32 %2, 10\\ns_mov_b32 %3, 11\\ns_mov_b32 %0, 12\\ns_mov_b32 %1, 13\\ns_mov_b32 %2, 14\\ns_mov_b32 %3, 15" : "=s"(d0_), "=s"(d1_), "=s"(d2_), "=s"(d3_)); }\n            __builtin_amdgcn_sched_barrier(0);\n')],
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
 }

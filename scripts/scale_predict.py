@@ -79,7 +79,7 @@ def group_solve_ms(reps=6):
     return [round(resident_ms(g, reps), 4) for g in range(1, 9)]
 
 
-def stream_prediction(n, solve_ms, pairs=64):
+def stream_prediction(n, solve_ms, pairs=64, link_gbps=None):
     """The stream leg at N ranks: rank 0 keeps pairs 0, N, 2N, ... and sends
     every other pair's two u8 frames to its owner; each rank's share goes in
     frame_parallel.group_sizes groups (the bench's rule, with the measured
@@ -87,17 +87,18 @@ def stream_prediction(n, solve_ms, pairs=64):
     pass (its groups' frames arriving over its link from rank 0, solves,
     (u, v) back over the other direction), rank 0's own share has no
     transfers.  The slowest rank sets the pass."""
+    link = LINK_GBPS if link_gbps is None else link_gbps
     per = pairs // n
     in_mb = 2 * 1080 * 1920 / 1e6        # two u8 frames
     out_mb = 2 * 1080 * 1920 * 4 / 1e6   # u, v in f32
-    sizes = fp.group_sizes(per, n, in_mb, out_mb, solve_ms, LINK_GBPS)
-    own = fp.group_sizes(per, 1, in_mb, out_mb, solve_ms, LINK_GBPS)
-    t0 = fp.pipeline_ms(own, in_mb, out_mb, solve_ms, LINK_GBPS, remote=False)
-    t0 = fp.pipeline_ms(sizes, in_mb, out_mb, solve_ms, LINK_GBPS, remote=False) \
+    sizes = fp.group_sizes(per, n, in_mb, out_mb, solve_ms, link)
+    own = fp.group_sizes(per, 1, in_mb, out_mb, solve_ms, link)
+    t0 = fp.pipeline_ms(own, in_mb, out_mb, solve_ms, link, remote=False)
+    t0 = fp.pipeline_ms(sizes, in_mb, out_mb, solve_ms, link, remote=False) \
         if n > 1 else t0
-    tr = fp.pipeline_ms(sizes, in_mb, out_mb, solve_ms, LINK_GBPS) if n > 1 else 0.0
+    tr = fp.pipeline_ms(sizes, in_mb, out_mb, solve_ms, link) if n > 1 else 0.0
     total = max(t0, tr)
-    return {"n": n, "pairs_per_rank": per, "group_sizes": sizes,
+    return {"n": n, "link_gbps": link, "pairs_per_rank": per, "group_sizes": sizes,
             "rank0_ms": round(t0, 3), "remote_rank_ms": round(tr, 3),
             "frames": "u8", "ms_per_pass": round(total, 3),
             "pairs_per_s": round(pairs / total * 1e3, 1)}
@@ -261,5 +262,22 @@ def main():
     print(json.dumps(res, indent=1))
 
 
+def link_table(rates=(25.0, 50.0, 100.0, 150.0)):
+    """The stream leg's model at N = 1 and 8 for several link rates, from the
+    committed batch solve times (frame_parallel.GROUP_SOLVE_MS; CPU only):
+    how much the measured link (bench.stream_leg, link_gbps_measured) can
+    move config 4's scaling."""
+    base = stream_prediction(1, fp.GROUP_SOLVE_MS)
+    out = []
+    for r in rates:
+        p8 = stream_prediction(8, fp.GROUP_SOLVE_MS, link_gbps=r)
+        p8["speedup_vs_n1"] = round(p8["pairs_per_s"] / base["pairs_per_s"], 2)
+        out.append(p8)
+    return {"n1": base, "n8_by_link": out}
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--link-table"]:
+        print(json.dumps(link_table(), indent=1))
+    else:
+        main()

@@ -84,12 +84,17 @@ def test_jacobi_kernel_selector():
         hsflow.set_jacobi_kernel(4)
         assert hsflow.jacobi_kernel_name(1080, 1920, 8, 5) == "hs_jacobi_strip_kernel"
         assert hsflow.jacobi_kernel_name(1080, 1920, 8, 3) == "hs_jacobi_strip_kernel"
-        # K4 is built for windows 3 and 5 at their default depth only
+        # K4 is built for window 3 at KB 8 and window 5 at KB 4, 5 and 6
         assert hsflow.jacobi_kernel_name(1080, 1920, 8, 7) == "hs_jacobi_wg_kernel"
         assert hsflow.jacobi_kernel_name(1080, 1920, 8, 2) == "hs_jacobi_kernel"
         assert hsflow.jacobi_kernel_name(1080, 1920, 8, 15) == "hs_jacobi_generic_kernel"
-        hsflow.set_iters_per_launch(4)  # a depth K4 is not built for: K2
+        for kb in (4, 5):
+            hsflow.set_iters_per_launch(kb)
+            assert hsflow.jacobi_kernel_name(1080, 1920, 8, 5) == "hs_jacobi_strip_kernel"
+        hsflow.set_iters_per_launch(3)  # a depth K4 is not built for: K2
         assert hsflow.jacobi_kernel_name(1080, 1920, 8, 5) == "hs_jacobi_wg_kernel"
+        hsflow.set_iters_per_launch(4)
+        assert hsflow.jacobi_kernel_name(1080, 1920, 8, 3) == "hs_jacobi_wg_kernel"
     finally:
         hsflow.set_iters_per_launch(0)
         hsflow.set_jacobi_kernel(0)
@@ -273,3 +278,20 @@ def test_kernel_choice_rules_for_partial_fills():
     }
     for (rows, cols, batch), name in cases.items():
         assert hsflow.jacobi_kernel_name(rows, cols, batch, 5) == name, (rows, cols, batch)
+
+
+def test_k4_segment_heights_for_partial_fills():
+    """K4 segment heights (w = 5): a single pair whose waves run alone on
+    their SIMDs takes the cost model's height, now also below 48 rows
+    (round 6, profiles/r06_kb_sweep.txt: a 1440p pair at 36 rows, 1000
+    waves, 15 % faster than at 48); the 4K pair keeps 84 (962 waves), the
+    batches 84, a 1080p pair runs K2 (0)."""
+    cases = {(1440, 2560, 1): 36, (2160, 3840, 1): 84, (1080, 1920, 8): 84,
+             (2160, 3840, 2): 84, (1080, 1920, 1): 0, (640, 7680, 1): 60}
+    for (rows, cols, batch), n in cases.items():
+        assert hsflow.strip_seg_rows(rows, cols, batch, 5) == n, (rows, cols, batch)
+    hsflow.set_strip_rows(48)
+    try:
+        assert hsflow.strip_seg_rows(2160, 3840, 1, 5) == 48
+    finally:
+        hsflow.set_strip_rows(0)

@@ -97,6 +97,12 @@ def test_bench_timing_and_stream_leg_over_gloo(world):
     assert leg0["frames"] == "u8" and sum(leg0["group_sizes"]) == len(range(0, N_PAIRS, world))
     assert leg0["parity"]["bitwise_vs_resident"] == {"pairs": N_PAIRS, "identical": N_PAIRS}
     assert leg0["parity"]["ok"]
+    # the link was measured before the timed passes (every peer of rank 0)
+    # and every rank sized its groups with the same broadcast rate
+    assert len(leg0["link_gbps_per_peer"]) == world - 1
+    assert all(x > 0 for x in leg0["link_gbps_per_peer"])
+    for r in range(world):
+        assert res[r][2]["link_gbps_model"] == leg0["link_gbps_model"] > 0
 
 
 def test_stream_leg_gathers_every_pair_in_order_one_rank():

@@ -179,6 +179,56 @@ def test_group_sizes_model():
     assert fp.pipeline_ms([5, 2, 1], 4.1, 16.6) < fp.pipeline_ms([5, 2, 1], 16.6, 16.6)
 
 
+@pytest.mark.parametrize("gbps", [25.0, 50.0, 100.0, 150.0])
+def test_group_sizes_follow_the_measured_link(gbps):
+    """bench.stream_leg sizes the groups with the link rate it measured
+    (frame_parallel.measure_link_gbps): valid non-increasing partitions at
+    any rate, never worse than the sizes picked for another rate, and a
+    faster link never makes the modelled pass slower."""
+    for share in (8, 16, 32):
+        s = fp.group_sizes(share, 8, 4.1, 16.6, link_gbps=gbps)
+        assert sum(s) == share and list(s) == sorted(s, reverse=True)
+        t = fp.pipeline_ms(s, 4.1, 16.6, link_gbps=gbps)
+        for other in (25.0, 50.0, 100.0, 150.0):
+            o = fp.group_sizes(share, 8, 4.1, 16.6, link_gbps=other)
+            assert t <= fp.pipeline_ms(o, 4.1, 16.6, link_gbps=gbps) + 1e-9
+        if gbps < 150.0:
+            faster = fp.group_sizes(share, 8, 4.1, 16.6, link_gbps=2 * gbps)
+            assert fp.pipeline_ms(faster, 4.1, 16.6, link_gbps=2 * gbps) <= t + 1e-9
+
+
+def _link_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.join(os.path.dirname(here), "cpp-optical-flow_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fp.measure_link_gbps(torch.device("cpu"), rank, world, 1 << 20)))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_measure_link_gbps_world3():
+    """Rank 0 times a round trip to each peer; every rank gets the slowest
+    peer's rate (broadcast), finite and positive."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_link_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+    assert isinstance(res[0], dict), res
+    assert len(res[0]["per_peer"]) == 2 and all(x > 0 for x in res[0]["per_peer"])
+    assert all(res[r]["link_gbps"] == res[0]["link_gbps"] for r in range(3))
+    assert abs(res[0]["link_gbps"] - min(res[0]["per_peer"])) <= 0.01 * res[0]["link_gbps"] + 0.01
+
+
 def test_pipelined_single_rank_groups():
     out = fp.run_stream_pipelined(_stream(), N_PAIRS, (ROWS, COLS), torch.float32,
                                   _solve_batch, torch.device("cpu"), 0, 1, chunks=3)

@@ -62,6 +62,25 @@ def test_k4_bits_equal_k2(hs, batch, rows, cols, w, iters):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
+@pytest.mark.parametrize("kb", [4, 5])
+@pytest.mark.parametrize("batch,rows,cols,iters,seg_rows", [
+    (1, 2, 3, 11, 0), (2, 37, 53, 13, 0), (1, 375, 1242, 100, 0), (2, 200, 257, 30, 16),
+    (1, 1080, 1920, 42, 40), (1, 2160, 3840, 20, 32), (3, 64, 131, 17, 24),
+])
+def test_k4_shallow_depths_bits_equal_k2(hs, kb, batch, rows, cols, iters, seg_rows):
+    """K4 built at KB 4 and 5 for w = 5 (fewer registers per wave: more
+    waves per SIMD for launches that fill part of the chip) gives K2's bits
+    too: odd widths, 1-row-ish planes, short segments, a shorter last pass."""
+    I0, I1 = _pairs(hs, batch, rows, cols)
+    hs.set_iters_per_launch(kb)
+    try:
+        a = _solve(hs, 2, I0, I1, 5, iters)
+        b = _solve(hs, 4, I0, I1, 5, iters, seg_rows=seg_rows)
+    finally:
+        hs.set_iters_per_launch(0)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("seg_rows", [12, 36, 84, 240])
 def test_k4_segment_height_invariance(hs, seg_rows):
     I0, I1 = _pairs(hs, 2, 257, 390)
