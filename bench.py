@@ -107,6 +107,12 @@ PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r05.json")
 # bands leg: coarse levels up to this many pixels are solved whole on every
 # rank (the 8K pyramid's 1920 x 1080 level 2; row_bands.whole_levels)
 BANDS_WHOLE_MAX_PX = 2_200_000
+# iterations between exchanges per level for the 2-D block split (N = 8
+# predicted 14.4 ms per 8K pair at 48,96 against 23.6 at 24,48: the
+# exchange's fixed cost dominates a 24-iteration chunk of a 2256 x 2112
+# block; profiles/r06_blocks_prediction.json)
+BLOCKS_CHUNK = "48,96"
+ROWS_CHUNK = "24,48"
 KERNEL_SOURCES = ("hsflow_strips.hip", "hsflow_kernels.hip", "hsflow_device.h")
 # measured VALU issue cost per wave64 instruction per SIMD (shader cycles)
 # at each Jacobi kernel's occupancy: profiles/r02_valu_tput.txt, mean of
@@ -160,11 +166,16 @@ def parse(argv=None):
                          "(the metric, plus the secondary / e2e / stream legs); stream: "
                          "BASELINE config 4 alone; bands: BASELINE config 5 on N GPUs, "
                          "ONE pair split into row bands with a halo exchange")
-    ap.add_argument("--chunk", default="24,48",
+    ap.add_argument("--chunk", default=None,
                     help="bands: iterations between halo exchanges, one value or one per "
                          "pyramid level from the finest (the last repeats): coarse levels "
                          "carry little work per chunk, so longer chunks there save "
-                         "exchanges")
+                         "exchanges (default 48,96 for blocks, 24,48 for row bands)")
+    ap.add_argument("--split", choices=["auto", "rows", "blocks"], default="auto",
+                    help="bands: how one pair is split over N ranks: row bands "
+                         "(row_bands.py) or a 2-D grid of blocks (blocks.py); auto = "
+                         "blocks (fewer halo pixels and bytes per exchange; "
+                         "scripts/scale_predict.py --blocks), rows with --overlap")
     ap.add_argument("--overlap", action="store_true",
                     help="bands mode: hide each exchange behind the next chunk's interior "
                          "(row_bands.solve_overlapped; bit-identical)")
@@ -1204,6 +1215,7 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     import torch.distributed as dist
     import hsflow
     import row_bands as rb
+    import blocks as bl
 
     wl = dict(WORKLOADS[args.workload if args.workload != "1080p" else "8k"])
     rows, cols = wl["rows"], wl["cols"]
@@ -1211,10 +1223,20 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     levels = args.levels or wl.get("levels", 1)
     in_dtype = args.dtype or wl.get("dtype", "f32")
     window, alpha = args.window, args.alpha
+    want_overlap = bool(args.overlap if overlap is None else overlap) and world > 1
+    # row bands or a grid of blocks (the overlapped schedule exists for bands)
+    split = getattr(args, "split", "auto") or "auto"
+    if split == "auto":
+        split = "rows" if (want_overlap or world == 1) else "blocks"
+    if split == "blocks" and want_overlap:
+        print("bench: bands --overlap runs row bands only; blocks without overlap",
+              file=sys.stderr)
+        want_overlap = False
     # one rank exchanges nothing: its band is the whole plane, solved in one
     # call per level
     if chunk is None:
-        chunk = ([int(x) for x in str(args.chunk).split(",")] if world > 1 else iters)
+        spec = args.chunk or (BLOCKS_CHUNK if split == "blocks" else ROWS_CHUNK)
+        chunk = ([int(x) for x in str(spec).split(",")] if world > 1 else iters)
     tdt = {"f16": torch.float16, "f32": torch.float32, "u8": torch.uint8}[in_dtype]
     I0 = torch.empty((rows, cols), dtype=tdt, device=dev)
     I1 = torch.empty_like(I0)
@@ -1226,37 +1248,50 @@ def bands_leg(args, world, rank, dev, steps, warmup, chunk=None, overlap=None, o
     if world > 1:
         dist.broadcast(I0, 0)
         dist.broadcast(I1, 0)
-    want_overlap = bool(args.overlap if overlap is None else overlap) and world > 1
     # the chunks asked for where their halos fit the bands, shorter where not
     # (e.g. --chunk 24,48 at 8 ranks with window 7); said on stderr
     # coarse levels of at most BANDS_WHOLE_MAX_PX solved whole on every rank:
     # no chunks, no exchanges (row_bands.whole_levels)
     whole = rb.whole_levels(rows, cols, levels, world, BANDS_WHOLE_MAX_PX)
-    p, notes = rb.fit_plan(rows, cols, levels, world, window, chunk, overlap=want_overlap,
-                           whole=whole)
+    if split == "blocks":
+        p, notes = bl.fit_plan2d(rows, cols, levels, world, window, chunk, whole=whole)
+    else:
+        p, notes = rb.fit_plan(rows, cols, levels, world, window, chunk, overlap=want_overlap,
+                               whole=whole)
     for msg in notes:
         print(f"bench: bands {msg}", file=sys.stderr)
     ops = [ops if ops is not None else rb.DeviceOps(window, alpha, dev)]
-    comm = rb.DistComm() if world > 1 else rb.LocalComm()
     res = [None]
 
-    overlap = want_overlap and rb.overlap_ok(p)
-    if want_overlap and not overlap:
-        print("bench: bands --overlap cannot be used with this plan; plain schedule",
-              file=sys.stderr)
-    solve = rb.solve_overlapped if overlap else rb.solve
+    if split == "blocks":
+        comm = bl.DistComm2D() if world > 1 else bl.LocalComm2D()
+        overlap = False
 
-    def one():
-        states = solve([I0], [I1], p, iters, ops, comm, [rank])
-        res[0] = rb.gather_owned(states, p, comm)
+        def one():
+            states = bl.solve([I0], [I1], p, iters, ops, comm, [rank])
+            res[0] = bl.gather_owned(states, p, comm)
+    else:
+        comm = rb.DistComm() if world > 1 else rb.LocalComm()
+        overlap = want_overlap and rb.overlap_ok(p)
+        if want_overlap and not overlap:
+            print("bench: bands --overlap cannot be used with this plan; plain schedule",
+                  file=sys.stderr)
+        solve = rb.solve_overlapped if overlap else rb.solve
+
+        def one():
+            states = solve([I0], [I1], p, iters, ops, comm, [rank])
+            res[0] = rb.gather_owned(states, p, comm)
 
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     elapsed = timed_region(one, sync, steps, warmup, world, dev)
     px_all = sum(r * c for r, c in p.sizes)
     exchanges = sum(-(-iters // c) for c, w in zip(p.chunks, p.whole) if not w) \
         if world > 1 else 0
+    shape = (f"a {p.grid[0]} x {p.grid[1]} grid of blocks" if split == "blocks" else
+             f"{world} row band" + ("s" if world > 1 else ""))
     leg = {"workload": f"{cols}x{rows} {in_dtype}, {levels} levels, {iters} it/level, "
-                       f"ws {window}, one pair in {world} row band" + ("s" if world > 1 else ""),
+                       f"ws {window}, one pair in {shape}",
+           "split": split + (f" {p.grid[0]}x{p.grid[1]}" if split == "blocks" else ""),
            "value": round(px_all * iters * steps / elapsed / 1e6, 1), "unit": "Mpix*iter/s",
            "ms_per_pair": round(elapsed / steps * 1e3, 3), "steps": steps,
            "pairs_per_s": round(steps / elapsed, 2),
@@ -1285,7 +1320,7 @@ def bands_mode(args, world, rank, dev):
     status = 0
     if rank == 0:
         print(json.dumps({
-            "metric": "Mpix*iter/s (config 5: one pair in row bands, halo exchange over RCCL)",
+            "metric": "Mpix*iter/s (config 5: one pair split over ranks, halo exchange over RCCL)",
             "value": leg["value"], "unit": "Mpix*iter/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": leg["ms_per_pair"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -1294,7 +1329,7 @@ def bands_mode(args, world, rank, dev):
                        "chunks_per_level": leg["chunks_per_level"],
                        "halo_rows_per_level": leg["halo_rows_per_level"],
                        "exchange": leg["exchange"],
-                       "parallelism": f"row bands x{world}"},
+                       "parallelism": f"{leg['split']} x{world}"},
             "parity": leg["parity"], "bands": leg}), flush=True)
         status = 3 if leg["parity"].get("ok") is False else 0
     if world > 1:

@@ -42,6 +42,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cpp-optical-flow_amd"), ROOT]
+import blocks as bl  # noqa: E402
 import frame_parallel as fp  # noqa: E402
 import hsflow  # noqa: E402
 import row_bands as rb  # noqa: E402
@@ -251,7 +252,61 @@ def bands_prediction(n, chunk=(24, 48), iters=1000, whole_px=2_200_000, overlap=
     return out
 
 
+def blocks_prediction(n, chunk=(24, 48), iters=1000, whole_px=2_200_000):
+    """The 2-D block split (blocks.py, bench.py --split blocks): per level
+    the largest extended block solved in chunks (GPU time measured on a
+    dense plane of that shape), each exchange XCHG_US of latency plus its
+    largest message (every peer on a link of its own: edges of H rows or
+    columns of u and v, corners) at LINK_GBPS, its host posting
+    XCHG_HOST_US per two peers (the bands' constant is for two); per chunk
+    the slower of the GPU and the host sets the pace.  Coarse levels of at
+    most whole_px pixels solved whole on every rank, as for the bands; the
+    gather moves the owned blocks (u, v) to rank 0 at LINK_GBPS."""
+    whole = rb.whole_levels(4320, 7680, 3, n, whole_px)
+    p, notes = bl.fit_plan2d(4320, 7680, 3, n, 5, chunk if n > 1 else iters, whole=whole)
+    own = max((b.b - b.a) * (b.d - b.c) for b in p.blocks[0]) * 8 / 1e6
+    gather = own / LINK_GBPS if n > 1 else 0.0
+    rec = {"n": n, "grid": list(p.grid), "chunks_per_level": list(p.chunks),
+           "halo_per_level": list(p.halos), "notes": notes, "gather_ms": round(gather, 3),
+           "levels": []}
+    total = gather
+    for l in range(p.levels - 1, -1, -1):
+        big = max(p.blocks[l], key=lambda b: (b.e1 - b.e0) * (b.f1 - b.f0))
+        R, C = big.shape()
+        if p.whole[l] or n == 1:
+            g, h, k1 = chunk_costs(R, C, iters, nchunks=3)
+            lvl = max(g, h) + k1
+            rec["levels"].append({"level": l, "block": [R, C], "whole": True,
+                                  "gpu_ms": round(g, 4), "ms": round(lvl, 3)})
+            total += lvl
+            continue
+        ck, H = p.chunks[l], p.halos[l]
+        g, h, k1 = chunk_costs(R, C, ck)
+        nch = -(-iters // ck)
+        peers = max(len(bl.halo_sources(p, l, r)) for r in range(n))
+        msg = max(max(H * (b.d - b.c), H * (b.b - b.a)) for b in p.blocks[l]) * 8 / 1e6
+        xfer = msg / LINK_GBPS
+        per = max(g + XCHG_US / 1e3 + xfer, h + XCHG_HOST_US / 1e3 * peers / 2)
+        lvl = nch * per + k1
+        rec["levels"].append({"level": l, "block": [R, C], "chunks": nch, "chunk": ck,
+                              "halo": H, "peers": peers, "gpu_ms_per_chunk": round(g, 4),
+                              "host_ms_per_chunk": round(h, 4),
+                              "exchange_transfer_ms": round(xfer, 4),
+                              "ms_per_chunk": round(per, 4), "ms": round(lvl, 3)})
+        total += lvl
+    rec["ms_per_pair"] = round(total, 2)
+    return rec
+
+
 def main():
+    if sys.argv[1:2] == ["--blocks"]:
+        chunks = [tuple(int(x) for x in c.split(",")) for c in (sys.argv[2:] or ["24,48"])]
+        print(json.dumps({"constants": {"LINK_GBPS": LINK_GBPS, "XCHG_US": XCHG_US,
+                                        "XCHG_HOST_US": XCHG_HOST_US},
+                          "blocks": [dict(whole_px=w, **blocks_prediction(n, c, whole_px=w))
+                                     for w in (2_200_000, 0) for c in chunks
+                                     for n in (2, 4, 8)]}, indent=1), flush=True)
+        return
     res = {"constants": {"LINK_GBPS": LINK_GBPS, "XCHG_US": XCHG_US,
                          "XCHG_HOST_US": XCHG_HOST_US},
            "resident_1080p_x8_ms": round(resident_ms(8), 3)}
@@ -259,6 +314,7 @@ def main():
     res["stream"] = [stream_prediction(n, gs) for n in (1, 2, 4, 8)]
     res["bands"] = [bands_prediction(n) for n in (1, 2, 4, 8)]
     res["bands_no_whole"] = [bands_prediction(n, whole_px=0, overlap=False) for n in (2, 4, 8)]
+    res["blocks"] = [blocks_prediction(n) for n in (2, 4, 8)]
     print(json.dumps(res, indent=1))
 
 

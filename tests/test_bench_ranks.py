@@ -119,7 +119,7 @@ def test_stream_leg_gathers_every_pair_in_order_one_rank():
 B_ROWS, B_COLS, B_LEVELS, B_ITERS, B_CHUNK = 104, 45, 2, 8, 3
 
 
-def _bands_worker(rank, world, port, q, overlap):
+def _bands_worker(rank, world, port, q, overlap, split="auto"):
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, ROOT, os.path.join(ROOT, "oracle"),
                     os.path.join(ROOT, "cpp-optical-flow_amd")]
@@ -132,7 +132,7 @@ def _bands_worker(rank, world, port, q, overlap):
                                         levels=B_LEVELS, dtype="f32")
         args = types.SimpleNamespace(workload="tinyb", iters=0, levels=0, dtype=None,
                                      window=5, alpha=1.0, chunk=B_CHUNK, overlap=overlap,
-                                     mode="resident")
+                                     mode="resident", split=split)
         out = []
         leg = bench.bands_leg(args, world, rank, torch.device("cpu"), steps=2, warmup=1,
                               ops=OracleOps(5, 1.0), result=out)
@@ -143,8 +143,8 @@ def _bands_worker(rank, world, port, q, overlap):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_bench_bands_leg_over_gloo(overlap):
+@pytest.mark.parametrize("overlap,split", [(False, "auto"), (False, "rows"), (True, "auto")])
+def test_bench_bands_leg_over_gloo(overlap, split):
     """bench.bands_leg -- the default run's configs[4] leg at N > 1 -- with 2
     ranks over gloo: frames broadcast from rank 0, row bands with the halo
     exchange after every chunk (the code RCCL runs), timed with the driver's
@@ -157,7 +157,7 @@ def test_bench_bands_leg_over_gloo(overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bands_worker, args=(r, world, port, q, overlap))
+    procs = [ctx.Process(target=_bands_worker, args=(r, world, port, q, overlap, split))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -173,6 +173,8 @@ def test_bench_bands_leg_over_gloo(overlap):
     # the coarse level (52 x 23 px) is small enough to be solved whole on
     # every rank (bench.BANDS_WHOLE_MAX_PX): exchanges only at level 0
     assert leg0["whole_levels"] == [1]
+    # auto: a grid of blocks (2 x 1 for this 104 x 45 frame), rows with --overlap
+    assert leg0["split"] == ("blocks 2x1" if split == "auto" and not overlap else "rows")
     assert leg0["exchanges_per_solve"] == -(-B_ITERS // B_CHUNK)
     assert leg0["chunks_per_level"] == [B_CHUNK] * B_LEVELS
     assert leg0["ms_per_pair"] == leg1["ms_per_pair"] > 0  # max over ranks
