@@ -942,7 +942,7 @@ def stream_leg(wl_name, args, world, rank, dev, solve_batch=None, n_pairs=None, 
     leg = {"pairs_per_s": round(n * steps / elapsed, 2),
            "ms_per_pass": round(elapsed / steps * 1e3, 3), "pairs": n,
            "groups_per_rank": len(my_sizes), "group_sizes": my_sizes,
-           "link_gbps_measured": (round(link["link_gbps"], 2) if link else None),
+           "link_gbps_measured": (round(link["measured_gbps"], 3) if link else None),
            "link_gbps_per_peer": (link["per_peer"] if link and rank == 0 else None),
            "link_gbps_model": round(link_gbps, 2),
            "frames": "u8",

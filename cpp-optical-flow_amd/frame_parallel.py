@@ -160,7 +160,9 @@ def measure_link_gbps(device, rank: int, world: int, nbytes: int, reps: int = 3)
     rate = nbytes / (best round trip / 2).  Rank 0 broadcasts the result, so
     every rank sizes its groups (group_sizes) with the same value: the
     slowest peer's rate (`link_gbps`), or LINK_GBPS if a measurement is not
-    finite and positive.  Returns {"link_gbps", "per_peer"} on every rank.
+    finite and positive, clamped to [1, 1000] for the model.  Returns
+    {"link_gbps" (the model's input), "measured_gbps", "per_peer"} on every
+    rank.
     Runs outside any timed region; one call costs ~2 reps (world - 1)
     transfers of nbytes (7 peers x 3 x 2 x 8.3 MB at 50 GB/s: ~7 ms)."""
     import time
@@ -198,7 +200,11 @@ def measure_link_gbps(device, rank: int, world: int, nbytes: int, reps: int = 3)
         rate = LINK_GBPS
     if not (rate > 0.0 and rate < float("inf")):
         rate = LINK_GBPS
-    return {"link_gbps": rate, "per_peer": [round(x, 2) for x in per_peer]}
+    # the schedule model's input stays within [1, 1000] GB/s (a host-side
+    # transport such as gloo over CUDA tensors measures ~0.03 GB/s, at which
+    # the model would cut every share into single pairs)
+    return {"link_gbps": min(max(rate, 1.0), 1000.0), "measured_gbps": rate,
+            "per_peer": [round(x, 3) for x in per_peer]}
 
 
 def pipeline_ms(sizes: Sequence[int], in_mb: float, out_mb: float,

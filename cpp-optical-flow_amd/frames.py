@@ -223,37 +223,100 @@ def consecutive_pairs(n_frames: int, start: int = 0, count: Optional[int] = None
     return [(j, j + gap) for j in idx]
 
 
+def pair_windows(pairs: Sequence[Tuple[int, int]], size: int) -> List[List[int]]:
+    """Indices of `pairs` cut into consecutive windows of at most `size`
+    pairs (the unit solve_stream reads, uploads and solves at a time)."""
+    size = max(1, int(size))
+    return [list(range(k, min(len(pairs), k + size))) for k in range(0, len(pairs), size)]
+
+
 def solve_stream(src, pairs: Sequence[Tuple[int, int]], window: int, iters: int,
-                 alpha: float, rank: int = 0, world: int = 1, device=None, gather=True):
-    """Frames -> pairs -> frame-parallel solve.  Rank 0 reads the frames
-    (host I/O), uploads them as 8-bit BGR or gray and converts BGR to gray
-    on the GPU; pairs are scattered round-robin over the ranks
-    (frame_parallel.run_stream), solved with hsflow.flow_device and (u, v)
-    gathered back in stream order on rank 0."""
+                 alpha: float, rank: int = 0, world: int = 1, device=None, gather=True,
+                 batch: int = 8, on_flow=None):
+    """Frames -> pairs -> frame-parallel solve (main.cpp:53-59 over a stream
+    of pairs).  The pairs go in windows of `batch` x world consecutive pairs:
+    rank 0 reads only the frames a window needs (frames two pairs share --
+    (j, j+1), (j+1, j+2) -- are read and converted once; the last frames
+    carry over to the next window), uploads them as 8-bit BGR or gray,
+    converts BGR to gray on the GPU (hsflow_bgr_to_gray_device), and the
+    window runs through frame_parallel.run_stream_pipelined: each rank's
+    share in batches of up to `batch` pairs (one batched flow_device call
+    each, the batch rate of the resident bench rather than the single-pair
+    one), scattered and gathered over torch.distributed when world > 1.
+    Frames and device buffers of a window are released before the next, so
+    device memory is bounded by the window, not by the video length.
+    Returns rank 0's (u, v) per pair in order (device tensors; None on other
+    ranks or when gather=False); with `on_flow(k, u, v)` each pair's flow is
+    handed over as its window finishes and nothing is kept (memory bounded
+    by one window of results too).  Bit-identical to one hsflow_flow call
+    per pair (K1, K2 and K4 give the same bits for any batch)."""
     import torch
     import frame_parallel as fp
     import hsflow
     device = device or torch.device("cuda", torch.cuda.current_device())
     shape = None
-    stream = None
-    if rank == 0:
-        gray = {}
-
-        def to_gray(i):
-            if i not in gray:
-                fr = torch.from_numpy(np.ascontiguousarray(src.read(i))).to(device)
-                gray[i] = hsflow.bgr_to_gray_device(fr) if fr.dim() == 3 else fr
-            return gray[i]
-        stream = [(to_gray(a), to_gray(b)) for a, b in pairs]
-        shape = tuple(stream[0][0].shape)
+    first = None
+    if rank == 0 and pairs:
+        first = src.read(pairs[0][0])
+        shape = tuple(first.shape[:2])
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor(list(shape) if shape else [0, 0], dtype=torch.int64, device=device)
         dist.broadcast(t, 0)
         shape = (int(t[0]), int(t[1]))
+    if not pairs:
+        return [] if gather and rank == 0 else None
+    rows, cols = shape
+    ws = {"t": None, "n": 0}
 
-    def solve(I0, I1):
-        u, v = hsflow.flow_device(I0, I1, window, iters, alpha)
-        return u, v
-    return fp.run_stream(stream, len(pairs), shape, torch.uint8, solve, device, rank, world,
-                         gather=gather)
+    def solve_batch(I0, I1):
+        n = I0.shape[0]
+        if ws["n"] < n:  # one workspace for the largest batch, reused
+            ws["t"] = hsflow.alloc_workspace(rows, cols, n, device)
+            ws["n"] = n
+        return hsflow.flow_device(I0, I1, window, iters, alpha, workspace=ws["t"])
+
+    in_mb, out_mb = 2 * rows * cols / 1e6, 2 * rows * cols * 4 / 1e6
+
+    def sizes(share):
+        return fp.group_sizes(share, world, in_mb, out_mb, cap=batch)
+
+    gray = {}
+
+    def to_gray(i):
+        nonlocal first
+        if i not in gray:
+            if first is not None and i == pairs[0][0]:  # read once, for the shape
+                img, first = first, None
+            else:
+                img = src.read(i)
+            x = torch.from_numpy(np.ascontiguousarray(img)).to(device)
+            g = hsflow.bgr_to_gray_device(x) if x.dim() == 3 else x
+            if tuple(g.shape) != shape:
+                raise FrameError("Image sizes are different")  # main.cpp:70-73
+            gray[i] = g
+        return gray[i]
+
+    out: List = []
+    wins = pair_windows(pairs, batch * max(1, world))
+    for w, idx in enumerate(wins):
+        stream = None
+        if rank == 0:
+            stream = [(to_gray(pairs[k][0]), to_gray(pairs[k][1])) for k in idx]
+        res = fp.run_stream_pipelined(stream, len(idx), shape, torch.uint8, solve_batch,
+                                      device, rank, world, gather=gather, sizes=sizes)
+        if rank == 0:
+            # keep only the frames a later window reads
+            later = ({f for k in wins[w + 1] for f in pairs[k]} if w + 1 < len(wins)
+                     else set())
+            for i in [i for i in gray if i not in later]:
+                del gray[i]
+            if gather and res is not None:
+                for k, (u, v) in zip(idx, res):
+                    if on_flow is not None:
+                        on_flow(k, u, v)
+                    else:
+                        out.append((u, v))
+    if rank != 0 or not gather:
+        return None
+    return None if on_flow is not None else out

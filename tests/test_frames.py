@@ -135,6 +135,14 @@ def test_capture_pair_and_consecutive_pairs(tmp_path):
     assert fr.consecutive_pairs(5, start=1, count=2, gap=2) == [(1, 3), (2, 4)]
 
 
+def test_pair_windows():
+    pairs = fr.consecutive_pairs(20)
+    w = fr.pair_windows(pairs, 8)
+    assert [len(x) for x in w] == [8, 8, 3]
+    assert sum(w, []) == list(range(19))
+    assert fr.pair_windows([], 8) == []
+
+
 # ----------------------------------------------------------------- GPU
 @pytest.mark.gpu
 def test_stream_of_bgr_frames_equals_per_pair_solves(tmp_path):
@@ -181,3 +189,59 @@ def test_y4m_stream_and_cpp_driver(tmp_path):
     assert np.array_equal(uc, ur.astype(np.float64))
     with pytest.raises(subprocess.CalledProcessError):
         subprocess.check_call([exe, p, "0", "7", out])   # frame 7 does not exist -> -1
+
+
+class _CountingSource:
+    """A source that counts its reads (solve_stream reads each frame once)."""
+
+    def __init__(self, frames):
+        self.frames, self.reads = frames, []
+
+    def __len__(self):
+        return len(self.frames)
+
+    def read(self, i):
+        self.reads.append(i)
+        return self.frames[i]
+
+
+@pytest.mark.gpu
+def test_kitti_y4m_stream_against_the_float64_oracle(tmp_path):
+    """main.cpp:53-59 over a video: the KITTI 000050 pair (the reference's
+    own frames, 15-bit gray fixtures) as a YUV4MPEG2 stream of 2 x 9 frames
+    (a, b, a, b, ...), every consecutive pair solved by solve_stream in
+    batched windows (8 pairs per batch: two windows, the second a partial
+    one) -- each (u, v) within the north_star tolerance (1e-4, norm-relative)
+    of the float64 oracle's restatement of hornSchunck.cpp, not of hsflow
+    itself; each frame read once."""
+    import torch
+    import oracle
+    from conftest import norm_rel_err
+    a = read_pgm(os.path.join(GOLDEN, "kitti_000050_10.pgm"))
+    b = read_pgm(os.path.join(GOLDEN, "kitti_000050_11.pgm"))
+    p = str(tmp_path / "kitti.y4m")
+    seq = [a, b] * 9
+    fr.write_y4m(p, seq, full_range=True)
+    src = _CountingSource([fr.Y4MVideo(p).read(i) for i in range(len(seq))])
+    pairs = fr.consecutive_pairs(len(src))
+    out = fr.solve_stream(src, pairs, 5, 100, 1.0, batch=8)
+    torch.cuda.synchronize()
+    assert len(out) == len(pairs) == 17
+    assert sorted(src.reads) == list(range(18))             # lazy: each frame once
+    ab = oracle.flow(a.astype(np.float64), b.astype(np.float64), 5, 100, 1.0)
+    ba = oracle.flow(b.astype(np.float64), a.astype(np.float64), 5, 100, 1.0)
+    for k, (u, v) in enumerate(out):
+        uo, vo = ab if k % 2 == 0 else ba
+        assert norm_rel_err(u.cpu().numpy(), uo) <= 1e-4, k
+        assert norm_rel_err(v.cpu().numpy(), vo) <= 1e-4, k
+    # the flow checksum of this pair (SURVEY §4.3, the float64 restatement
+    # that reproduces the reference's arrow plot pixel-exactly)
+    assert abs(float(ab[0].sum()) - (-9517.890763654887)) < 1e-6
+    assert abs(float(out[0][0].double().sum()) - float(ab[0].sum())) < 0.05
+    # on_flow: the flows handed over window by window, nothing kept
+    got = {}
+    assert fr.solve_stream(src, pairs[:10], 5, 100, 1.0, batch=4,
+                           on_flow=lambda k, u, v: got.__setitem__(k, u.clone())) is None
+    assert sorted(got) == list(range(10))
+    for k in range(10):
+        assert torch.equal(got[k], out[k][0])
