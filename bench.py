@@ -41,7 +41,7 @@ timed replays themselves computed (u, v); a parity miss anywhere exits 3.
                 packed gradients, write u, v: 20 B per pixel; the first pass
                 reads no u, v) / avg_launch_ms, frac = achieved / 8 TB/s (a
                 physical fraction, <= 1); traffic = PMC bytes per pass of the
-                timed configuration (profiles/pmc_r05.json, rocprofv3 --pmc of
+                timed configuration (profiles/pmc_r06.json, rocprofv3 --pmc of
                 scripts/timed_step.py), hbm_frac = traffic / avg_launch_ms /
                 8 TB/s.  `isolated_launch`: one single-stream launch timed
                 with events on its stream (what rocprofv3 reports per
@@ -103,7 +103,7 @@ NAIVE_BYTES_PER_PX_ITER = 28  # f32 u, v, Ix, Iy, It in, u', v' o
 PARITY_TOL = 1e-4          # north_star: 1e-4 relative (norm form)
 GOLDEN_JSON = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 GOLDEN_NPZ = os.path.join(ROOT, "tests", "golden", "bench_golden.npz")
-PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r05.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "pmc_r06.json")
 # bands leg: coarse levels up to this many pixels are solved whole on every
 # rank (the 8K pyramid's 1920 x 1080 level 2; row_bands.whole_levels)
 BANDS_WHOLE_MAX_PX = 2_200_000
@@ -369,7 +369,7 @@ def kernel_source_md5():
 
 
 def pmc_for(wl_name, window, batch, kb, kernel, timed=False, passes=None):
-    """Committed PMC summary of this roofline leg (profiles/pmc_r05.json,
+    """Committed PMC summary of this roofline leg (profiles/pmc_r06.json,
     written by scripts/pmc_collect.py from separate rocprofv3 --pmc passes)
     if it was collected for this kernel, blocking depth, batch and kernel
     source.  timed: the timed configuration's entry (scripts/timed_step.py:

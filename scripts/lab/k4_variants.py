@@ -111,9 +111,9 @@ PATCHES = {
     # -- stages KB/2.. take the level-(KB/2) sums of the PREVIOUS step -- so
     # a lone wave has two independent dependency chains per step: is the
     # single-pair launch latency-bound on the serial stage chain?
-    "split": [('    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n', "    f2v chu = {0.f, 0.f}, chv = {0.f, 0.f};\n" + '    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n'),
+    "split": [('    auto block = [&](int tb, auto rowe_c, auto fill_c, auto plain_c) {\n', "    f2v chu = {0.f, 0.f}, chv = {0.f, 0.f};\n" + '    auto block = [&](int tb, auto rowe_c, auto fill_c, auto plain_c) {\n'),
               ('                if (kf < 2 * AR * j) break;  // nor any later stage\n', '                if (kf < 2 * AR * j) break;  // nor any later stage\n' + "                if (j == KB / 2) { const f2v a0 = hu, a1 = hv; hu = chu; hv = chv; chu = a0; chv = a1; }\n")],
-    "split3": [('    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n', "    f2v chu = {0.f, 0.f}, chv = {0.f, 0.f}, dhu = {0.f, 0.f}, dhv = {0.f, 0.f};\n" + '    auto block = [&](int tb, auto rowe_c, auto fill_c) {\n'),
+    "split3": [('    auto block = [&](int tb, auto rowe_c, auto fill_c, auto plain_c) {\n', "    f2v chu = {0.f, 0.f}, chv = {0.f, 0.f}, dhu = {0.f, 0.f}, dhv = {0.f, 0.f};\n" + '    auto block = [&](int tb, auto rowe_c, auto fill_c, auto plain_c) {\n'),
                ('                if (kf < 2 * AR * j) break;  // nor any later stage\n', '                if (kf < 2 * AR * j) break;  // nor any later stage\n' + "                if (j == 2) { const f2v a0 = hu, a1 = hv; hu = chu; hv = chv; chu = a0; chv = a1; }\n"
                          "                if (j == 4) { const f2v a0 = hu, a1 = hv; hu = dhu; hv = dhv; dhu = a0; dhv = a1; }\n")],
     # timing only: no memory traffic (every load / store out of range, the
@@ -133,10 +133,21 @@ PATCHES = {
 }
 
 
+# variants that are another variant's source compiled with other scheduler
+# options: name -> (source variant, extra hipcc flags)
+FLAG_VARIANTS = {
+    "ilp": ("base", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+    "split3ilp": ("split3", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+    "iilp": ("base", ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]),
+    "split3iilp": ("split3", ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]),
+}
+
+
 def build(name):
     os.makedirs(LAB, exist_ok=True)
     src = open(SRC).read()
-    for old, new in PATCHES[name]:
+    base, extra = FLAG_VARIANTS.get(name, (name, []))
+    for old, new in PATCHES[base]:
         assert old in src, (name, old)
         src = src.replace(old, new)
     path = os.path.join(PKG, "csrc", f"_lab_strips_{name}.hip")
@@ -144,7 +155,7 @@ def build(name):
         f.write(src)
     obj = os.path.join(LAB, f"strips_{name}.o")
     try:
-        subprocess.check_call(["/opt/rocm/bin/hipcc", *FLAGS, "-c", path, "-o", obj])
+        subprocess.check_call(["/opt/rocm/bin/hipcc", *FLAGS, *extra, "-c", path, "-o", obj])
     finally:
         os.remove(path)
     objs = [os.path.join(PKG, "build", f) for f in sorted(os.listdir(os.path.join(PKG, "build")))

@@ -160,7 +160,7 @@ def test_pmc_profile_used_only_for_the_kernel_source_it_was_collected_on(tmp_pat
 
 
 def test_committed_pmc_profile_matches_the_kernel_sources():
-    """profiles/pmc_r05.json (what the bench's roofline reads) was collected
+    """profiles/pmc_r06.json (what the bench's roofline reads) was collected
     on the current Jacobi kernel sources, for the timed step of the headline
     and 4K legs as well as the single-stream launches; its timed-step bytes
     per pass are physical (the step's HBM traffic within 1.3x the
