@@ -302,7 +302,7 @@ def prewarm(step, sync, seconds=PREWARM_S, max_steps=400):
     """Untimed steps until `seconds` of load have passed, before the W
     warm-up steps: the GPU needs ~0.1 s under load to reach its steady
     clocks (same box, 1080p x 8: 2 warm-up steps read 1.22-1.24 M, 20 read
-    1.33 M, 60 1.34 M), so a short driver warm-up would time
+    1.33 M, 60 1.34 M; profiles/HISTORY.md), so a short driver warm-up would time
     the clock ramp, not the kernels.  Returns (steps, seconds) run."""
     sync()
     t0 = time.perf_counter()
@@ -687,7 +687,7 @@ def e2e_leg(wl_name, args, dev, n_batches=48, slots=3):
     first upload) and drain (the last 2.4 ms download) are paid once per
     stream, as a video would pay them; with 12 batches they were 10 % of
     the time (rocprofv3 trace of scripts/e2e_probe.py: 4.6 ms per solve with
-    the downloads running beside it against 4.3 ms alone)."""
+    the downloads running beside it against 4.3 ms alone, profiles/HISTORY.md)."""
     import numpy as np
     import torch
     import hsflow
