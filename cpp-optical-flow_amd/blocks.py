@@ -258,47 +258,90 @@ class LocalComm2D:
 
 
 class DistComm2D:
-    """torch.distributed point-to-point: to every rank s whose extended block
-    overlaps ours, the part of our owned block it needs (a dense copy); from
-    every rank that owns part of our halo, that part into a receive buffer,
-    copied in after the requests complete.  Messages go in (field, peer)
-    order on both ends, so RCCL's in-order matching per peer pairs them.
-    Under RCCL every step is stream-ordered on the current stream; gloo
-    moves host-side, so the send copies are fenced first."""
+    """torch.distributed point-to-point: to every rank q whose extended block
+    overlaps ours, the part of our owned block it needs; from every rank
+    that owns part of our halo, that part.  One message per peer and
+    direction carries both fields (u and v stacked), so an exchange posts
+    2 x peers operations (5 peers at N = 8).  Device tensors: the send and
+    receive buffers of a level are allocated once and reused by every
+    chunk (stream order keeps that safe: RCCL's requests are waited for on
+    the current stream before the next chunk stacks into them), the sends
+    are packed with one stack per peer and the receives unpacked with one
+    fused copy.  Messages go in peer order on both ends, so RCCL's
+    in-order matching per peer pairs them.  Under gloo (host-side
+    transport) the send buffers are fenced first."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def _plan(self, s, level):
+        """Per level: [(peer, send rect (local slices) or None, recv rect
+        (local slices), recv shape)] in peer order."""
+        p, r = s.plan, s.rank
+        me = p.blocks[level][r]
+        out = []
+        for q, rect_in in halo_sources(p, level, r):
+            rect_out = overlap(me.own(), p.blocks[level][q].ext())
+            out.append((q, None if rect_out is None else local(me, rect_out),
+                        local(me, rect_in), (rect_in[1] - rect_in[0], rect_in[3] - rect_in[2])))
+        return out
 
     def exchange(self, states: Sequence["BlockState"], level: int):
         import torch
         import torch.distributed as dist
         (s,) = states
-        p, r = s.plan, s.rank
-        me = p.blocks[level][r]
-
-        def t(x):
-            return torch.from_numpy(x) if isinstance(x, np.ndarray) else x
-        ops, unpack, sends = [], [], []
-        # peers: ranks we send to (their extended block overlaps our owned one)
-        # are exactly the ranks we receive from (the overlap is symmetric for a
-        # grid with one halo width)
-        peers = [(q, rect) for q, rect in halo_sources(p, level, r)]
-        for f in (s.u[level], s.v[level]):
-            for q, rect_in in peers:
-                qb = p.blocks[level][q]
-                rect_out = overlap(me.own(), qb.ext())
-                if rect_out is not None:
-                    sb = _crop(s.ops, f, *[x - o for x, o in zip(rect_out, (me.e0, me.e0,
-                                                                            me.f0, me.f0))])
+        u, v = s.u[level], s.v[level]
+        plan = self._plan(s, level)
+        ops, sends = [], []
+        if isinstance(u, np.ndarray):
+            recvs = []
+            for q, so, si, shape in plan:
+                if so is not None:
+                    sb = torch.from_numpy(np.ascontiguousarray(np.stack((u[so], v[so]))))
                     sends.append(sb)
-                    ops.append(dist.P2POp(dist.isend, t(sb), q))
-                rr0, rr1, cc0, cc1 = rect_in
-                buf = (np.empty((rr1 - rr0, cc1 - cc0), dtype=f.dtype) if isinstance(f, np.ndarray)
-                       else torch.empty((rr1 - rr0, cc1 - cc0), dtype=f.dtype, device=f.device))
-                ops.append(dist.P2POp(dist.irecv, t(buf), q))
-                unpack.append((f, local(me, rect_in), buf))
+                    ops.append(dist.P2POp(dist.isend, sb, q))
+                rb_ = torch.from_numpy(np.empty((2,) + shape, dtype=u.dtype))
+                recvs.append((si, rb_))
+                ops.append(dist.P2POp(dist.irecv, rb_, q))
+            for req in (dist.batch_isend_irecv(ops) if ops else []):
+                req.wait()
+            for si, rb_ in recvs:
+                u[si] = rb_[0].numpy()
+                v[si] = rb_[1].numpy()
+            return
+        key = (level, u.device, u.dtype, u.shape)
+        if key not in self._bufs:
+            bufs = []
+            for q, so, si, shape in plan:
+                sbuf = None
+                if so is not None:
+                    h = so[0].stop - so[0].start
+                    w = so[1].stop - so[1].start
+                    sbuf = torch.empty((2, h, w), dtype=u.dtype, device=u.device)
+                bufs.append((sbuf, torch.empty((2,) + shape, dtype=u.dtype, device=u.device)))
+            self._bufs = {key: bufs}     # one level at a time
+        bufs = self._bufs[key]
+        ctx = s.ops._on() if hasattr(s.ops, "_on") else None
+        import contextlib
+        with ctx if ctx is not None else contextlib.nullcontext():
+            for (q, so, si, shape), (sbuf, rbuf) in zip(plan, bufs):
+                if so is not None:
+                    torch.stack((u[so], v[so]), out=sbuf)
+                    sends.append(sbuf)
         rb.host_transport_fence(sends)
+        for (q, so, si, shape), (sbuf, rbuf) in zip(plan, bufs):
+            if sbuf is not None:
+                ops.append(dist.P2POp(dist.isend, sbuf, q))
+            ops.append(dist.P2POp(dist.irecv, rbuf, q))
         for req in (dist.batch_isend_irecv(ops) if ops else []):
             req.wait()
-        for f, sl, buf in unpack:
-            f[sl] = buf
+        dsts, srcs = [], []
+        for (q, so, si, shape), (sbuf, rbuf) in zip(plan, bufs):
+            dsts += [u[si], v[si]]
+            srcs += [rbuf[0], rbuf[1]]
+        if dsts:
+            with ctx if ctx is not None else contextlib.nullcontext():
+                torch._foreach_copy_(dsts, srcs)
 
 
 # ------------------------------------------------------------------ solver
