@@ -309,6 +309,14 @@ class DistComm2D:
                 u[si] = rb_[0].numpy()
                 v[si] = rb_[1].numpy()
             return
+        # RCCL orders its work against the CURRENT stream: a rank whose work
+        # runs on a stream of its own (DeviceOps(stream=...)) has the current
+        # stream wait for it before posting, and its stream wait for the
+        # transfers and the unpack afterwards (as row_bands.DistComm)
+        rank_stream = getattr(s.ops, "stream", None)
+        cur = torch.cuda.current_stream(u.device)
+        if rank_stream is not None:
+            cur.wait_stream(rank_stream)
         key = (level, u.device, u.dtype, u.shape)
         if key not in self._bufs:
             bufs = []
@@ -321,13 +329,10 @@ class DistComm2D:
                 bufs.append((sbuf, torch.empty((2,) + shape, dtype=u.dtype, device=u.device)))
             self._bufs = {key: bufs}     # one level at a time
         bufs = self._bufs[key]
-        ctx = s.ops._on() if hasattr(s.ops, "_on") else None
-        import contextlib
-        with ctx if ctx is not None else contextlib.nullcontext():
-            for (q, so, si, shape), (sbuf, rbuf) in zip(plan, bufs):
-                if so is not None:
-                    torch.stack((u[so], v[so]), out=sbuf)
-                    sends.append(sbuf)
+        for (q, so, si, shape), (sbuf, rbuf) in zip(plan, bufs):
+            if so is not None:
+                torch.stack((u[so], v[so]), out=sbuf)   # on the current stream
+                sends.append(sbuf)
         rb.host_transport_fence(sends)
         for (q, so, si, shape), (sbuf, rbuf) in zip(plan, bufs):
             if sbuf is not None:
@@ -340,8 +345,9 @@ class DistComm2D:
             dsts += [u[si], v[si]]
             srcs += [rbuf[0], rbuf[1]]
         if dsts:
-            with ctx if ctx is not None else contextlib.nullcontext():
-                torch._foreach_copy_(dsts, srcs)
+            torch._foreach_copy_(dsts, srcs)
+        if rank_stream is not None:
+            rank_stream.wait_stream(cur)
 
 
 # ------------------------------------------------------------------ solver
