@@ -33,6 +33,19 @@ PATCHES = {
                 ("                f2v Tr;\n", ""),
                 ("                op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);",
                  "                X[r] = f2v{ixe, ixo}; Y[r] = f2v{iye, iyo}; T[r] = f2v{ite, ito};")],
+    # timing only (wrong results): every launch runs 2x / 4x its iterations
+    # in the same workgroup lifetime (the halo is too shallow for them), so
+    # the solve-time difference is the iteration sweep alone -- how much of
+    # a single-pair launch the per-launch load / set-up / store / launch gap
+    # costs (round 6, the register-resident persistent-kernel question)
+    "it2": [("    const int n_it = p.iters;\n    for (int it = 0;",
+             "    const int n_it = p.iters * 2;\n    for (int it = 0;"),
+            ("    const int n_it = p.iters;\n    // The vertical",
+             "    const int n_it = p.iters * 2;\n    // The vertical")],
+    "it4": [("    const int n_it = p.iters;\n    for (int it = 0;",
+             "    const int n_it = p.iters * 4;\n    for (int it = 0;"),
+            ("    const int n_it = p.iters;\n    // The vertical",
+             "    const int n_it = p.iters * 4;\n    // The vertical")],
 }
 
 
