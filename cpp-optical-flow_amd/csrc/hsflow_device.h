@@ -183,11 +183,22 @@ __device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) {
     return __builtin_elementwise_fma(a, b, c);
 }
 
-__device__ __forceinline__ void op_setup(float alpha2, float ixe, float iye, float ite,
+// alpha^2 of a lane's column pair: alpha^2 inside the image, 1 outside.  A
+// column outside the image reads zero gradients, so its operator is
+// X = Y = T = 0 * rsq(alpha^2): 0 for any alpha but 0 * inf = NaN at
+// alpha = 0, and that NaN would reach the image through the next
+// iteration's window sums (the reference never computes those columns:
+// hornSchunck.cpp:60-61 pads with zeros).  With 1 there they stay exactly
+// 0; columns inside the image keep the caller's alpha^2 (same bits).
+__device__ __forceinline__ f2v alpha2_cols(float alpha2, bool ce, bool co) {
+    return f2v{ce ? alpha2 : 1.f, co ? alpha2 : 1.f};
+}
+
+__device__ __forceinline__ void op_setup(f2v alpha2, float ixe, float iye, float ite,
                                          float ixo, float iyo, float ito, f2v &X, f2v &Y,
                                          f2v &T) {
-    const float se = __builtin_amdgcn_rsqf(fmaf_x(iye, iye, fmaf_x(ixe, ixe, alpha2)));
-    const float so = __builtin_amdgcn_rsqf(fmaf_x(iyo, iyo, fmaf_x(ixo, ixo, alpha2)));
+    const float se = __builtin_amdgcn_rsqf(fmaf_x(iye, iye, fmaf_x(ixe, ixe, alpha2.x)));
+    const float so = __builtin_amdgcn_rsqf(fmaf_x(iyo, iyo, fmaf_x(ixo, ixo, alpha2.y)));
     X = f2v{ixe * se, ixo * so};
     Y = f2v{iye * se, iyo * so};
     T = f2v{ite * se, ito * so};

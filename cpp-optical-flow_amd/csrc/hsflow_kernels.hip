@@ -643,6 +643,14 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
     // window-mean factor of this lane's columns: 1/w^2 inside the image, 0 outside
     const f2v colm = {ce ? p.inv_w2 : 0.f, co ? p.inv_w2 : 0.f};
     const int ce_i = ce ? 1 : 0, co_i = co ? 1 : 0;
+    // Border tiles zero the columns outside the image either by per-lane
+    // selects after the update (SEL: w >= 8, whose factor form spills) or by
+    // the window-mean factor 0 there.  The factor form needs the operator of
+    // those columns to be 0, not NaN: alpha^2 per column, 1 outside the
+    // image (hsflow_device.h alpha2_cols; w = 6 then spills 8 bytes, still
+    // fewer than with the selects).  Interior tiles have no column outside.
+    constexpr bool SEL = EDGE && W >= 8;
+    const f2v a2c = (EDGE && !SEL) ? alpha2_cols(p.alpha2, ce, co) : f2v{p.alpha2, p.alpha2};
     uint64_t rowmask = 0;
 #pragma unroll
     for (int r = 0; r < RW; ++r)
@@ -727,10 +735,10 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
             }
             if constexpr (TL) {
                 f2v Tr;
-                op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], Tr);
+                op_setup(a2c, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], Tr);
                 tw[r * 64] = make_float2(Tr.x, Tr.y);
             } else {
-                op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);
+                op_setup(a2c, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);
             }
         }
     }
@@ -922,9 +930,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                     }
                 }
                 f2v nu, nv;
-                if constexpr (EDGE && W >= 8) {
+                if constexpr (SEL) {
                     // outside the image u = v = 0 (BORDER_CONSTANT); per-lane
-                    // selects (the factor form below spills at W = 8, 9)
+                    // selects (see SEL)
                     op_update(su, sv, invv, X[y], Y[y], t_row(y), nu, nv);
                     const bool rin = (rowmask >> y) & 1ull;
                     const bool ie = rin & (launder(ce_i) != 0);

@@ -160,7 +160,7 @@ __device__ __forceinline__ void load_row(RowIn<G32> &d, const Rsrc &rs, int vo_e
 // operations per column -- fma(Ix, Ix, alpha^2), fma(Iy, Iy, .), rsq, three
 // products -- so the same bits, in half the instructions
 template <bool G32>
-__device__ __forceinline__ void row_op(float alpha2, const RowIn<G32> &d, f2v &X, f2v &Y,
+__device__ __forceinline__ void row_op(f2v a2, const RowIn<G32> &d, f2v &X, f2v &Y,
                                        f2v &T) {
     f2v ix, iy, it;
     if constexpr (G32) {
@@ -170,7 +170,6 @@ __device__ __forceinline__ void row_op(float alpha2, const RowIn<G32> &d, f2v &X
     } else {
         unpack_grad_pair(d.g.x, d.g.y, ix, iy, it);
     }
-    const f2v a2 = {alpha2, alpha2};
     const f2v den = fma2(iy, iy, fma2(ix, ix, a2));
     const f2v sc = {__builtin_amdgcn_rsqf(den.x), __builtin_amdgcn_rsqf(den.y)};
     X = ix * sc;
@@ -208,6 +207,8 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     // window-mean factor of this lane's columns: 1/w^2 inside the image, 0
     // outside (there the loaded gradients are 0 too, so the update is 0)
     const f2v colm = {ce ? p.inv_w2 : 0.f, co ? p.inv_w2 : 0.f};
+    // alpha^2 per column, 1 outside the image (hsflow_device.h alpha2_cols)
+    const f2v a2c = alpha2_cols(p.alpha2, ce, co);
     const int c4 = gce * 4;
     // per-lane load offsets (the row goes in soffset); X2: one 8-byte word
     // per column pair, wholly inside or outside the image (even width)
@@ -235,7 +236,6 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
     rs.vo = __builtin_amdgcn_make_buffer_rsrc((void *)(p.v_out + pbase), 0, plane_bytes,
                                               0x00020000);
 
-    const float alpha2 = p.alpha2;
     // The stream: rows a - KB A .. b - 1 + KB AR, downwards (dir = 1) from
     // an even first row (segment starts are even, and so is KB A) or upwards
     // (dir = -1) from an odd first row -- one more row streamed when b - 1 +
@@ -388,7 +388,7 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                 }
             }
             // 4. operator of row t, into the slot stage KB has just read
-            row_op<G32>(alpha2, cur, OX[k % L], OY[k % L], OT[k % L]);
+            row_op<G32>(a2c, cur, OX[k % L], OY[k % L], OT[k % L]);
             __builtin_amdgcn_sched_barrier(0);
         }
     };

@@ -27,11 +27,11 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fno-slp-vector
 
 PATCHES = {
     "base": [],
-    "nosetup": [("                op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], Tr);",
+    "nosetup": [("                op_setup(a2c, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], Tr);",
                  "                X[r] = f2v{ixe, ixo}; Y[r] = f2v{iye, iyo}; f2v Tr = f2v{ite, ito};"
-                 " (void)p.alpha2;"),
+                 " (void)a2c;"),
                 ("                f2v Tr;\n", ""),
-                ("                op_setup(p.alpha2, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);",
+                ("                op_setup(a2c, ixe, iye, ite, ixo, iyo, ito, X[r], Y[r], T[r]);",
                  "                X[r] = f2v{ixe, ixo}; Y[r] = f2v{iye, iyo}; T[r] = f2v{ite, ito};")],
     # timing only (wrong results): every launch runs 2x / 4x its iterations
     # in the same workgroup lifetime (the halo is too shallow for them), so

@@ -117,6 +117,39 @@ def test_all_window_sizes(hs, ctx, w):
     assert norm_rel_err(u, uo) <= TOL and norm_rel_err(v, vo) <= TOL
 
 
+@pytest.mark.parametrize("kernel", [0, 2, 4])  # automatic, K2 tiles, K4 strips (w 3, 5)
+@pytest.mark.parametrize("w", [3, 5, 6, 9])
+def test_alpha_zero_nan_pattern_matches_the_oracle(hs, w, kernel):
+    """alpha = 0 is a legal hornSchunck argument.  The reference then divides
+    by Ix^2 + Iy^2 (hornSchunck.cpp:63-68), which is 0 at every image corner
+    (reflect-101 Sobel: Ix = 0 on the first and last column, Iy on the first
+    and last row), so NaN appears there and spreads through the window sums.
+    The GPU must give NaN exactly where the oracle does and match it
+    elsewhere: the strip/tile columns outside the image must stay 0, not
+    0 * rsq(0) = NaN (hsflow_device.h alpha2_cols)."""
+    import torch
+    I0, I1 = hs.synth_pair(321, 70, 300)  # several K4 strips / K2 tiles across
+    uo, vo = _oracle_flow(I0, I1, w, 6, alpha=0.0)
+    assert not np.isfinite(uo).all() and np.isfinite(uo).mean() > 0.5
+    hs.set_jacobi_kernel(kernel)
+    try:
+        # a batch of two (the K4 batch rules) and the single pair
+        t0 = torch.from_numpy(np.stack([I0, I0])).cuda()
+        t1 = torch.from_numpy(np.stack([I1, I1])).cuda()
+        ub, vb = hs.flow_device(t0, t1, w, 6, 0.0)
+        torch.cuda.synchronize()
+        us, vs = hs.flow_device(t0[:1], t1[:1], w, 6, 0.0)
+        torch.cuda.synchronize()
+    finally:
+        hs.set_jacobi_kernel(0)
+    for got_u, got_v in ((ub[0], vb[0]), (ub[1], vb[1]), (us[0], vs[0])):
+        for got, ref in ((got_u.cpu().numpy(), uo), (got_v.cpu().numpy(), vo)):
+            fin = np.isfinite(ref)
+            assert np.array_equal(np.isfinite(got), fin)
+            d = np.abs(got[fin].astype(np.float64) - ref[fin])
+            assert d.max() / np.abs(ref[fin]).max() <= TOL
+
+
 def test_zero_iterations_gives_zero_flow(hs, ctx, crop_small):
     u, v = ctx.flow(crop_small["I0"], crop_small["I1"], 5, 0, 1.0)
     assert not u.any() and not v.any()
