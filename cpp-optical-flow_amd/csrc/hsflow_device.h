@@ -215,4 +215,18 @@ __device__ __forceinline__ void op_update(f2v su, f2v sv, f2v invv, f2v X, f2v Y
     nv = fma2(-Y, k, vb);
 }
 
+// The same update from the window means themselves (ub, vb).  Windows 3
+// and 5 (K2 and K4) form the mean inside the vertical sum: the core that
+// two neighbouring rows share (w = 5: M = Q + Q, four rows; w = 3: the pair
+// sum Q) is scaled once, c M, and each row's mean is one fused
+// multiply-add with its remaining row h, ub = fma(h, c, c M) -- one packed
+// op per row and field fewer than S = h + M, ub = S c (a lone K4 wave's
+// time follows its packed-op count: profiles/r06_k4_nomul_ab.txt).
+__device__ __forceinline__ void op_update_mean(f2v ub, f2v vb, f2v X, f2v Y, f2v T, f2v &nu,
+                                               f2v &nv) {
+    const f2v k = fma2(X, ub, fma2(Y, vb, T));
+    nu = fma2(-X, k, ub);
+    nv = fma2(-Y, k, vb);
+}
+
 }  // namespace hsflow

@@ -876,43 +876,54 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
             } else {
                 hrow(t, hu[sl], hv[sl]);
             }
-            // pair sum Q(t-1) (w = 5: t-1 odd; w = 3: t-1 even; else every row)
+            // window-mean factors of this lane's columns (0 outside the
+            // image in border tiles)
+            const f2v cf = (EDGE && !SEL) ? launder_v2(colm) : invv;
+            // pair sum Q(t-1) (w = 5: t-1 odd; w = 3: t-1 even, kept as
+            // c Q, the core two rows' means share; else every row)
             if (rr >= 1 && (!SHARED || ((PAR + t - 1 + 2 * W) & 1) == (W == 5 ? 1 : 0))) {
                 const int sp = (t - 1 + 2 * W) % W;
-                qu[sp] = hu[sp] + hu[sl];
-                qv[sp] = hv[sp] + hv[sl];
+                if constexpr (W == 3) {
+                    qu[sp] = (hu[sp] + hu[sl]) * cf;
+                    qv[sp] = (hv[sp] + hv[sl]) * cf;
+                } else {
+                    qu[sp] = hu[sp] + hu[sl];
+                    qv[sp] = hv[sp] + hv[sl];
+                }
             }
             const int y = t - AR;  // slab row whose window ends at t
             if (y >= 0) {
-                // other windows: pair tree over rows y-A .. y+AR,
+                // w = 3, 5: the window means (ub, vb) straight from the
+                // scaled core, one fma per row (op_update_mean); other
+                // windows: pair tree over rows y-A .. y+AR,
                 // ((q(y-A) + q(y-A+2)) + ...) [+ h(y+AR) for odd W]
                 f2v su, sv;
                 const bool yev = ((PAR + y + 2 * W) & 1) == 0;  // image row y even
                 if constexpr (W == 5) {
                     const int s0 = (y - 2 + 2 * W) % W, s1 = (y - 1 + 2 * W) % W,
                               s2 = (y + 1 + 2 * W) % W, s3 = (y + 2 + 2 * W) % W;
-                    if (yev) {  // S(y) = h(y-2) + (Q(y-1) + Q(y+1))
-                        mu = qu[s1] + qu[s2];
-                        mv = qv[s1] + qv[s2];
-                        su = hu[s0] + mu;
-                        sv = hv[s0] + mv;
-                    } else {  // S(y) = (Q(y-2) + Q(y)) + h(y+2)
+                    if (yev) {  // mean(y): h(y-2) and c M(y), M(y) = Q(y-1) + Q(y+1)
+                        mu = (qu[s1] + qu[s2]) * cf;
+                        mv = (qv[s1] + qv[s2]) * cf;
+                        su = fma2(hu[s0], cf, mu);
+                        sv = fma2(hv[s0], cf, mv);
+                    } else {  // mean(y): c M(y-1), M(y-1) = Q(y-2) + Q(y), and h(y+2)
                         if (y == 0) {  // core M(-1) not formed by row -1
-                            mu = qu[s0] + qu[(y + 2 * W) % W];
-                            mv = qv[s0] + qv[(y + 2 * W) % W];
+                            mu = (qu[s0] + qu[(y + 2 * W) % W]) * cf;
+                            mv = (qv[s0] + qv[(y + 2 * W) % W]) * cf;
                         }
-                        su = mu + hu[s3];
-                        sv = mv + hv[s3];
+                        su = fma2(hu[s3], cf, mu);
+                        sv = fma2(hv[s3], cf, mv);
                     }
                 } else if constexpr (W == 3) {
                     const int s0 = (y - 1 + 2 * W) % W, s1 = (y + 2 * W) % W,
                               s2 = (y + 1 + 2 * W) % W;
-                    if (yev) {  // S(y) = h(y-1) + Q(y)
-                        su = hu[s0] + qu[s1];
-                        sv = hv[s0] + qv[s1];
-                    } else {  // S(y) = Q(y-1) + h(y+1)
-                        su = qu[s0] + hu[s2];
-                        sv = qv[s0] + hv[s2];
+                    if (yev) {  // mean(y): h(y-1) and c Q(y)
+                        su = fma2(hu[s0], cf, qu[s1]);
+                        sv = fma2(hv[s0], cf, qv[s1]);
+                    } else {  // mean(y): c Q(y-1) and h(y+1)
+                        su = fma2(hu[s2], cf, qu[s0]);
+                        sv = fma2(hv[s2], cf, qv[s0]);
                     }
                 } else {
                     su = qu[(y - A + 2 * W) % W];
@@ -929,11 +940,18 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                         sv = sv + hv[sh];
                     }
                 }
+                // (su, sv): window sums, or for w = 3, 5 already the means
+                auto update = [&](f2v factor, f2v T_y, f2v &nu_, f2v &nv_) {
+                    if constexpr (SHARED)
+                        op_update_mean(su, sv, X[y], Y[y], T_y, nu_, nv_);
+                    else
+                        op_update(su, sv, factor, X[y], Y[y], T_y, nu_, nv_);
+                };
                 f2v nu, nv;
                 if constexpr (SEL) {
                     // outside the image u = v = 0 (BORDER_CONSTANT); per-lane
                     // selects (see SEL)
-                    op_update(su, sv, invv, X[y], Y[y], t_row(y), nu, nv);
+                    update(invv, t_row(y), nu, nv);
                     const bool rin = (rowmask >> y) & 1ull;
                     const bool ie = rin & (launder(ce_i) != 0);
                     const bool io = rin & (launder(co_i) != 0);
@@ -947,7 +965,7 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                     // gradients read there are 0 (out-of-range loads), so the
                     // update yields 0 (every value in the region is finite)
                     // without per-lane masks.  Rows (wave-uniform): select.
-                    op_update(su, sv, launder_v2(colm), X[y], Y[y], t_row(y), nu, nv);
+                    update(cf, t_row(y), nu, nv);
                     if (ROWE && !((rowmask >> y) & 1ull)) {
                         nu = f2v{0.f, 0.f};
                         nv = f2v{0.f, 0.f};
@@ -958,9 +976,9 @@ __device__ __forceinline__ void wg_body_p(const JacobiArgs &p,
                     // keep the read of row y+1 here: only LDS reads may not
                     // be moved across (VALU, SALU, VMEM and DS writes may)
                     __builtin_amdgcn_sched_barrier(0x67E);
-                    op_update(su, sv, invv, X[y], Y[y], tcur, nu, nv);
+                    update(invv, tcur, nu, nv);
                 } else {
-                    op_update(su, sv, invv, X[y], Y[y], t_row(y), nu, nv);
+                    update(invv, t_row(y), nu, nv);
                 }
                 U[y] = nu;
                 V[y] = nv;

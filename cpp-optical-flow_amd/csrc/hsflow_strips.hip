@@ -26,9 +26,10 @@
 // The per-pixel operation sequence is K2's (hsflow_kernels.hip): the same
 // horizontal sums (hsum_c2, association by column parity), the same
 // vertical sums by image-row parity (w = 5: pair sums Q at odd rows, cores
-// M at even rows; w = 3: Q at even rows) and the same normalised update
-// (op_setup / op_update), so K4 and K2 give identical bits for every pass,
-// and a solve may mix them (K2 runs the passes K4 does not cover).
+// M at even rows; w = 3: Q at even rows), the same window means formed from
+// the scaled core (one fma per row) and the same normalised update
+// (op_setup / op_update_mean), so K4 and K2 give identical bits for every
+// pass, and a solve may mix them (K2 runs the passes K4 does not cover).
 //
 // Outside the image u = v = 0 (BORDER_CONSTANT, hornSchunck.cpp:60-61):
 // columns through the window-mean factor (0 outside, as in K2's border
@@ -69,45 +70,50 @@ constexpr int kOOB = 0x7FFFFFF0;
 // the alternation makes neighbouring segments read their shared halo rows
 // at the same time -- 4K x 2 +2.1 %, profiles/r05_k4_alt_dir_ab.txt).
 //
+// Each arrival returns the completed row's window MEAN (c = the lane's
+// window-mean factors): the shared core is scaled once and the row's mean
+// is fma(h, c, c core) (hsflow_device.h op_update_mean; K2 does the same).
+//
 // w = 5.  State before an even arrival t: e0 = h(t-4), e1 = h(t-2),
-// q = Q(t-3), x = h(t-1); before an odd arrival: x = M(t-3).
+// q = Q(t-3), x = h(t-1); before an odd arrival: x = c M(t-3).
 struct VS5 {
     f2v e0, e1, q, x;
 };
 template <int PT>  // PT: parity of the arriving image row t
-__device__ __forceinline__ f2v vs_arrive(VS5 &s, f2v h) {
+__device__ __forceinline__ f2v vs_arrive(VS5 &s, f2v h, f2v c) {
     if constexpr (PT == 0) {
         const f2v qn = s.x + h;  // Q(t-1) = h(t-1) + h(t)
         const f2v m = s.q + qn;  // M(t-2) = Q(t-3) + Q(t-1)
-        const f2v S = s.e0 + m;  // S(t-2) = h(t-4) + M(t-2)
+        const f2v mc = m * c;
+        const f2v ub = fma2(s.e0, c, mc);  // mean(t-2): h(t-4) and M(t-2)
         s.e0 = s.e1;
         s.e1 = h;
         s.q = qn;
-        s.x = m;
-        return S;
+        s.x = mc;
+        return ub;
     } else {
-        const f2v S = s.x + h;  // S(t-2) = M(t-3) + h(t)
+        const f2v ub = fma2(h, c, s.x);  // mean(t-2): M(t-3) and h(t)
         s.x = h;
-        return S;
+        return ub;
     }
 }
 // w = 3.  State before an odd arrival t: h1 = h(t-1), h2 = h(t-2); before
-// an even arrival: q = Q(t-2).
+// an even arrival: q = c Q(t-2).
 struct VS3 {
     f2v h1, h2, q;
 };
 template <int PT>
-__device__ __forceinline__ f2v vs_arrive(VS3 &s, f2v h) {
+__device__ __forceinline__ f2v vs_arrive(VS3 &s, f2v h, f2v c) {
     if constexpr (PT == 1) {
-        const f2v qn = s.h1 + h;  // Q(t-1) = h(t-1) + h(t)
-        const f2v S = s.h2 + qn;  // S(t-1) = h(t-2) + Q(t-1)
-        s.q = qn;
+        const f2v qc = (s.h1 + h) * c;     // c Q(t-1), Q(t-1) = h(t-1) + h(t)
+        const f2v ub = fma2(s.h2, c, qc);  // mean(t-1): h(t-2) and Q(t-1)
+        s.q = qc;
         s.h2 = h;
-        return S;
+        return ub;
     } else {
-        const f2v S = s.q + h;  // S(t-1) = Q(t-2) + h(t)
+        const f2v ub = fma2(h, c, s.q);  // mean(t-1): Q(t-2) and h(t)
         s.h1 = h;
-        return S;
+        return ub;
     }
 }
 
@@ -331,17 +337,17 @@ __device__ __forceinline__ void strip_body(const JacobiArgs &p, size_t pbase, in
                 // image-row parity of the arriving row t - j AR (tb even;
                 // upwards: flipped, tb odd -- the same pattern)
                 const int pt = (k + j * AR) & 1;
-                f2v Su, Sv;
+                f2v ub, vb;
                 if (pt == 0) {
-                    Su = vs_arrive<0>(su[j], hu);
-                    Sv = vs_arrive<0>(sv[j], hv);
+                    ub = vs_arrive<0>(su[j], hu, colm);
+                    vb = vs_arrive<0>(sv[j], hv, colm);
                 } else {
-                    Su = vs_arrive<1>(su[j], hu);
-                    Sv = vs_arrive<1>(sv[j], hv);
+                    ub = vs_arrive<1>(su[j], hu, colm);
+                    vb = vs_arrive<1>(sv[j], hv, colm);
                 }
                 const int sl = ((k - (j + 1) * AR) % L + L) % L;  // operator slot of row y
                 f2v nu, nv;
-                op_update(Su, Sv, colm, OX[sl], OY[sl], OT[sl], nu, nv);
+                op_update_mean(ub, vb, OX[sl], OY[sl], OT[sl], nu, nv);
                 if constexpr (ROWE) {
                     if ((unsigned)y >= (unsigned)rows) {  // rows outside the image: 0
                         nu = z;

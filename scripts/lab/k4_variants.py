@@ -128,6 +128,131 @@ PATCHES = {
     "valu16": [('            __builtin_amdgcn_sched_barrier(0);\n', '            { int d0_, d1_, d2_, d3_; asm volatile("v_mov_b32 %0, 0\\nv_mov_b32 %1, 1\\nv_mov_b32 %2, 2\\nv_mov_b32 %3, 3\\nv_mov_b32 %0, 4\\nv_mov_b32 %1, 5\\nv_mov_b32 %2, 6\\nv_mov_b32 %3, 7\\nv_mov_b32 %0, 8\\nv_mov_b32 %1, 9\\nv_mov_b32 %2, 10\\nv_mov_b32 %3, 11\\nv_mov_b32 %0, 12\\nv_mov_b32 %1, 13\\nv_mov_b32 %2, 14\\nv_mov_b32 %3, 15" : "=v"(d0_), "=v"(d1_), "=v"(d2_), "=v"(d3_)); }\n            __builtin_amdgcn_sched_barrier(0);\n')],
     "pk16": [('            __builtin_amdgcn_sched_barrier(0);\n', '            { f2v d0_, d1_, d2_, d3_; asm volatile("v_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4\\nv_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4\\nv_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4\\nv_pk_add_f32 %0, %4, %4\\nv_pk_add_f32 %1, %4, %4\\nv_pk_add_f32 %2, %4, %4\\nv_pk_add_f32 %3, %4, %4" : "=v"(d0_), "=v"(d1_), "=v"(d2_), "=v"(d3_) : "v"(colm)); }\n            __builtin_amdgcn_sched_barrier(0);\n')],
     "salu16": [('            __builtin_amdgcn_sched_barrier(0);\n', '            { int d0_, d1_, d2_, d3_; asm volatile("s_mov_b32 %0, 0\\ns_mov_b32 %1, 1\\ns_mov_b32 %2, 2\\ns_mov_b32 %3, 3\\ns_mov_b32 %0, 4\\ns_mov_b32 %1, 5\\ns_mov_b32 %2, 6\\ns_mov_b32 %3, 7\\ns_mov_b32 %0, 8\\ns_mov_b32 %1, 9\\ns_mov_b32 %2, 10\\ns_mov_b32 %3, 11\\ns_mov_b32 %0, 12\\ns_mov_b32 %1, 13\\ns_mov_b32 %2, 14\\ns_mov_b32 %3, 15" : "=s"(d0_), "=s"(d1_), "=s"(d2_), "=s"(d3_)); }\n            __builtin_amdgcn_sched_barrier(0);\n')],
+    # launches of lone waves (write-through ones, under 3/4 of the wave
+    # slots) ask for 40 KB of LDS per wave they do not use: at most 4
+    # workgroups per CU, so the dispatcher cannot put two of the launch's
+    # waves on one SIMD while another SIMD idles
+    "lds40": [("hs_jacobi_strip_kernel<W, KB, C::D, C::U, C::WPE, true>), grd,\n                           dim3(64), 0, s, a);",
+               "hs_jacobi_strip_kernel<W, KB, C::D, C::U, C::WPE, true>), grd,\n                           dim3(64), 40960, s, a);")],
+    # timing record (lab only): each wave of a K4 launch stores its start
+    # and end (s_memrealtime, 100 MHz), its hardware id (XCC, SE, CU, SIMD)
+    # and its segment / strip into a module array that
+    # hsflow_lab_k4_stamps() copies out (the last K4 launch's waves)
+    "stamp": [("#pragma clang fp contract(off)\n",
+               "#pragma clang fp contract(off)\n"
+               "__device__ unsigned long long g_k4_stamps[16384 * 4];\n"
+               "extern \"C\" int hsflow_lab_k4_stamps(void *host, int n) {\n"
+               "    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_k4_stamps),\n"
+               "                                    (size_t)n * 32, 0, hipMemcpyDeviceToHost);\n"
+               "}\n"),
+              ("    const int dir = (seg & 1) ? -1 : 1;\n    if (g32) {",
+               "    const int dir = (seg & 1) ? -1 : 1;\n"
+               "    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();\n"
+               "    if (g32) {"),
+              ("            strip_body<W, KB, D, U, false, false, WT>(p, pbase, plane_bytes, c0, a, b, dir);\n    }\n}",
+               "            strip_body<W, KB, D, U, false, false, WT>(p, pbase, plane_bytes, c0, a, b, dir);\n    }\n"
+               "    {\n"
+               "        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();\n"
+               "        unsigned hw = 0, xcc = 0;\n"
+               "        asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\" : \"=s\"(hw));\n"
+               "        asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\" : \"=s\"(xcc));\n"
+               "        if ((threadIdx.x & 63) == 0 && lin < 16384) {\n"
+               "            g_k4_stamps[4 * lin] = t_start;\n"
+               "            g_k4_stamps[4 * lin + 1] = t_end;\n"
+               "            g_k4_stamps[4 * lin + 2] = ((unsigned long long)xcc << 32) | hw;\n"
+               "            g_k4_stamps[4 * lin + 3] = ((unsigned long long)seg << 32) | (unsigned)sx;\n"
+               "        }\n"
+               "    }\n"
+               "}")],
+    # timing only (wrong values): the update without the two window-mean
+    # products per stage (12 fewer packed multiplies per time step): does
+    # a lone wave's time follow its instruction count?
+    "nomul": [("                op_update(Su, Sv, colm, OX[sl], OY[sl], OT[sl], nu, nv);",
+               "                {\n"
+               "                    const f2v k_ = fma2(OX[sl], Su, fma2(OY[sl], Sv, OT[sl]));\n"
+               "                    nu = fma2(-OX[sl], k_, Su);\n"
+               "                    nv = fma2(-OY[sl], k_, Sv);\n"
+               "                }")],
+    # timing only (wrong values): the horizontal sums as plain adds (the
+    # same count, no cross-lane DPP operand): what the DPP form costs
+    "nodpp": [("    hsum_c2<W>(u.x, u.y, v.x, v.y, a, b, c, d);",
+               "    {\n"
+               "        const float pu = u.x + u.y, pv = v.x + v.y;\n"
+               "        const float au = launder_f(pu + u.y), av = launder_f(pv + v.y);\n"
+               "        const float bu = launder_f(u.x + pu), bv = launder_f(v.x + pv);\n"
+               "        a = launder_f(au + u.x); c = launder_f(av + v.x);\n"
+               "        b = launder_f(bu + pu); d = launder_f(bv + pv);\n"
+               "    }")],
+    # timing only (wrong at the image's side columns): the window-mean
+    # factor uniform over the wave, so the compiler can take it from an SGPR
+    # pair (op_sel_hi) instead of a VGPR pair in the packed multiply-adds
+    "csgpr": [("    const f2v colm = {ce ? p.inv_w2 : 0.f, co ? p.inv_w2 : 0.f};",
+               "    const f2v colm = {p.inv_w2, p.inv_w2};")],
+    # timing record (lab only): lane 0 of every wave stores the shader
+    # clock (s_memtime) at the start of each unrolled block of its stream
+    # and at its end, slots [lin][0..15] of a module array that
+    # hsflow_lab_k4_bstamps() copies out (the last K4 launch's waves)
+    "bstamp": [("#pragma clang fp contract(off)\n",
+                "#pragma clang fp contract(off)\n"
+                "__device__ unsigned long long g_k4_bstamps[16384 * 16];\n"
+                "extern \"C\" int hsflow_lab_k4_bstamps(void *host, int n) {\n"
+                "    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_k4_bstamps),\n"
+                "                                    (size_t)n * 128, 0, hipMemcpyDeviceToHost);\n"
+                "}\n"),
+               ("    auto block = [&](int tb, auto rowe_c, auto fill_c, auto plain_c) {\n",
+                "    auto block = [&](int tb, auto rowe_c, auto fill_c, auto plain_c) {\n"
+                "        {\n"
+                "            const int bi_ = (tb - t_first) * dir / U;\n"
+                "            const unsigned long long ts_ = __builtin_amdgcn_s_memtime();\n"
+                "            if (lane == 0 && blockIdx.x < 16384 && bi_ < 15)\n"
+                "                g_k4_bstamps[blockIdx.x * 16 + bi_] = ts_;\n"
+                "        }\n"),
+               ("    for (; ib < nblk; tb += dir * U, ++ib) block(tb, std::true_type{}, F0{}, NP{});\n}",
+                "    for (; ib < nblk; tb += dir * U, ++ib) block(tb, std::true_type{}, F0{}, NP{});\n"
+                "    {\n"
+                "        const unsigned long long ts_ = __builtin_amdgcn_s_memtime();\n"
+                "        if (lane == 0 && blockIdx.x < 16384) g_k4_bstamps[blockIdx.x * 16 + 15] = ts_ | ((unsigned long long)nblk << 56);\n"
+                "    }\n"
+                "}")],
+    # the pipeline fill's two blocks as iterations of the row-zeroing loop
+    # body (every stage runs from the stream's first step, as before round
+    # 5's fill skipping; the same bits): the fill then runs code the wave
+    # re-uses instead of ~24 steps of straight-line code fetched once per
+    # wave -- is the fill's slowness at full chip instruction fetch?
+    "nofill": [("    block(tb, std::true_type{}, std::integral_constant<int, 1>{}, NP{});\n"
+                "    tb += dir * U;\n"
+                "    block(tb, std::true_type{}, std::integral_constant<int, 2>{}, NP{});\n"
+                "    tb += dir * U;\n",
+                "    for (int f_ = 0; f_ < 2; ++f_, tb += dir * U)\n"
+                "        block(tb, std::true_type{}, F0{}, NP{});\n")],
+    # the waves dispatched after one per SIMD (blockIdx.x >= 1024, the
+    # second wave of a SIMD in a full-chip launch) start their stream 6 or
+    # 12 us late, so the two waves' fills (memory-bound, 2.5x the steady
+    # step time when every wave of the chip fills at once) do not overlap
+    "stag4": [("    const int dir = (seg & 1) ? -1 : 1;\n",
+                "    const int dir = (seg & 1) ? -1 : 1;\n"
+                "    if (blockIdx.x >= 1024) {\n"
+                "        const long t0_ = wall_clock64();\n"
+                "        while (wall_clock64() - t0_ < 400) __builtin_amdgcn_s_sleep(8);\n"
+                "    }\n")],
+    "stag8": [("    const int dir = (seg & 1) ? -1 : 1;\n",
+                "    const int dir = (seg & 1) ? -1 : 1;\n"
+                "    if (blockIdx.x >= 1024) {\n"
+                "        const long t0_ = wall_clock64();\n"
+                "        while (wall_clock64() - t0_ < 800) __builtin_amdgcn_s_sleep(8);\n"
+                "    }\n")],
+    "stag12": [("    const int dir = (seg & 1) ? -1 : 1;\n",
+                "    const int dir = (seg & 1) ? -1 : 1;\n"
+                "    if (blockIdx.x >= 1024) {\n"
+                "        const long t0_ = wall_clock64();\n"
+                "        while (wall_clock64() - t0_ < 1200) __builtin_amdgcn_s_sleep(8);\n"
+                "    }\n")],
+    "stag16": [("    const int dir = (seg & 1) ? -1 : 1;\n",
+                "    const int dir = (seg & 1) ? -1 : 1;\n"
+                "    if (blockIdx.x >= 1024) {\n"
+                "        const long t0_ = wall_clock64();\n"
+                "        while (wall_clock64() - t0_ < 1600) __builtin_amdgcn_s_sleep(8);\n"
+                "    }\n")],
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
 }
@@ -143,13 +268,18 @@ FLAG_VARIANTS = {
 }
 
 
+# variants that stack other variants' patches: name -> patch names
+COMBOS = {"nofillbs": ["nofill", "bstamp"]}
+
+
 def build(name):
     os.makedirs(LAB, exist_ok=True)
     src = open(SRC).read()
     base, extra = FLAG_VARIANTS.get(name, (name, []))
-    for old, new in PATCHES[base]:
-        assert old in src, (name, old)
-        src = src.replace(old, new)
+    for pname in COMBOS.get(base, [base]):
+        for old, new in PATCHES[pname]:
+            assert old in src, (name, old)
+            src = src.replace(old, new)
     path = os.path.join(PKG, "csrc", f"_lab_strips_{name}.hip")
     with open(path, "w") as f:
         f.write(src)
