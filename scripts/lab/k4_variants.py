@@ -253,6 +253,12 @@ PATCHES = {
                 "        const long t0_ = wall_clock64();\n"
                 "        while (wall_clock64() - t0_ < 1600) __builtin_amdgcn_s_sleep(8);\n"
                 "    }\n")],
+    # prefetch depth 4 / 6 rows at w = 5 with one wave per SIMD's register
+    # budget (the lone-wave launches: 4K pair), current source
+    "d4w1": [("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12, WPE = 2; };",
+               "template <> struct StripCfg<5, 6> { static constexpr int D = 4, U = 12, WPE = 1; };")],
+    "d6w1": [("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12, WPE = 2; };",
+               "template <> struct StripCfg<5, 6> { static constexpr int D = 6, U = 12, WPE = 1; };")],
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
 }
@@ -269,7 +275,7 @@ FLAG_VARIANTS = {
 
 
 # variants that stack other variants' patches: name -> patch names
-COMBOS = {"nofillbs": ["nofill", "bstamp"]}
+COMBOS = {"nofillbs": ["nofill", "bstamp"], "d6w1bs": ["d6w1", "bstamp"]}
 
 
 def build(name):
