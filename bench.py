@@ -113,7 +113,8 @@ BANDS_WHOLE_MAX_PX = 2_200_000
 # block; profiles/r06_blocks_prediction.json)
 BLOCKS_CHUNK = "48,96"
 ROWS_CHUNK = "24,48"
-KERNEL_SOURCES = ("hsflow_strips.hip", "hsflow_kernels.hip", "hsflow_device.h")
+# (relative to csrc/; the Makefile carries the per-file scheduler flags)
+KERNEL_SOURCES = ("hsflow_strips.hip", "hsflow_kernels.hip", "hsflow_device.h", "../Makefile")
 # measured VALU issue cost per wave64 instruction per SIMD (shader cycles)
 # at each Jacobi kernel's occupancy: profiles/r02_valu_tput.txt, mean of
 # v_add / v_add_dpp / v_pk_add / v_fma / v_pk_fma at 2 (K4) and 4 (K2)

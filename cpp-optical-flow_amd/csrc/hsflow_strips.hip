@@ -185,10 +185,21 @@ __device__ __forceinline__ void row_op(f2v a2, const RowIn<G32> &d, f2v &X, f2v 
 
 template <int W>
 __device__ __forceinline__ void hrow(f2v u, f2v v, f2v &hu, f2v &hv) {
-    float a, b, c, d;
-    hsum_c2<W>(u.x, u.y, v.x, v.y, a, b, c, d);
-    hu = f2v{a, b};
-    hv = f2v{c, d};
+    if constexpr (W == 5) {
+        // hsum_c2's sums without its launder statements (empty asm, which
+        // the hazard recogniser pads with s_nops; K4's registers do not
+        // need them): the same operations, the same bits
+        const float pu = u.x + u.y, pv = v.x + v.y;
+        const float au = from_left(pu) + pu, av = from_left(pv) + pv;
+        const float bu = from_left(u.y) + pu, bv = from_left(v.y) + pv;
+        hu = f2v{au + from_right(u.x), bu + from_right(pu)};
+        hv = f2v{av + from_right(v.x), bv + from_right(pv)};
+    } else {
+        float a, b, c, d;
+        hsum_c2<W>(u.x, u.y, v.x, v.y, a, b, c, d);
+        hu = f2v{a, b};
+        hv = f2v{c, d};
+    }
 }
 
 }  // namespace

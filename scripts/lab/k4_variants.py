@@ -31,7 +31,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 PKG = os.path.join(ROOT, "cpp-optical-flow_amd")
 LAB = os.path.join(PKG, "lab")
 SRC = os.path.join(PKG, "csrc", "hsflow_strips.hip")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fno-slp-vectorize"]
+# the product build of hsflow_strips.hip (cpp-optical-flow_amd/Makefile STRIPS_FLAGS)
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fno-slp-vectorize",
+         "-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 
 PATCHES = {
     "base": [],
@@ -259,6 +261,15 @@ PATCHES = {
                "template <> struct StripCfg<5, 6> { static constexpr int D = 4, U = 12, WPE = 1; };")],
     "d6w1": [("template <> struct StripCfg<5, 6> { static constexpr int D = 3, U = 12, WPE = 2; };",
                "template <> struct StripCfg<5, 6> { static constexpr int D = 6, U = 12, WPE = 1; };")],
+    # the operator set-up of row t first in the step (into temporaries,
+    # written to its ring slot after stage KB has read it): independent
+    # work ahead of the stage chain for the scheduler to interleave
+    "ropfirst": [("            // 2. level-0 horizontal sums of row t\n",
+                  "            f2v rX_, rY_, rT_;\n"
+                  "            row_op<G32>(a2c, cur, rX_, rY_, rT_);\n"
+                  "            // 2. level-0 horizontal sums of row t\n"),
+                 ("            row_op<G32>(a2c, cur, OX[k % L], OY[k % L], OT[k % L]);\n",
+                  "            OX[k % L] = rX_;\n            OY[k % L] = rY_;\n            OT[k % L] = rT_;\n")],
     "sb2": [("            __builtin_amdgcn_sched_barrier(0);\n        }\n    };",
              "            if (k % 2 == 1) __builtin_amdgcn_sched_barrier(0);\n        }\n    };")],
 }
@@ -268,6 +279,7 @@ PATCHES = {
 # options: name -> (source variant, extra hipcc flags)
 FLAG_VARIANTS = {
     "ilp": ("base", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+    "ropfirstilp": ("ropfirst", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
     "split3ilp": ("split3", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
     "iilp": ("base", ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]),
     "split3iilp": ("split3", ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]),
@@ -310,9 +322,10 @@ hsflow.LIB_PATH = %(lib)r
 import numpy as np, torch
 out = {}
 SHAPES = {"1080p8": (8, 1080, 1920, 300), "4k2": (2, 2160, 3840, 500),
-          "4k1": (1, 2160, 3840, 500), "1080p1": (1, 1080, 1920, 300)}
+          "4k1": (1, 2160, 3840, 500), "1080p1": (1, 1080, 1920, 300),
+          "1080p8w3": (8, 1080, 1920, 300, 3), "1440p1": (1, 1440, 2560, 300)}
 for tag in os.environ.get("K4_SHAPES", "1080p8,4k2").split(","):
-    batch, rows, cols, iters = SHAPES[tag]
+    batch, rows, cols, iters, win = (SHAPES[tag] + (5,))[:5]
     ps = [hsflow.synth_pair(1000 + i, rows, cols) for i in range(batch)]
     I0 = torch.from_numpy(np.stack([p[0] for p in ps])).cuda()
     I1 = torch.from_numpy(np.stack([p[1] for p in ps])).cuda()
@@ -320,11 +333,11 @@ for tag in os.environ.get("K4_SHAPES", "1080p8,4k2").split(","):
     ws = hsflow.alloc_workspace(rows, cols, batch)
     s = torch.cuda.Stream(); s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws, s)
+        hsflow.flow_device(I0, I1, win, iters, 1.0, u, v, ws, s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with hsflow.max_streams_as(2), torch.cuda.graph(g, capture_error_mode="thread_local"):
-        hsflow.flow_device(I0, I1, 5, iters, 1.0, u, v, ws, torch.cuda.current_stream())
+        hsflow.flow_device(I0, I1, win, iters, 1.0, u, v, ws, torch.cuda.current_stream())
     t = time.perf_counter(); n = 0
     while time.perf_counter() - t < 0.15:
         g.replay(); n += 1
