@@ -29,6 +29,10 @@ SHAPES = [  # (name, batch, rows, cols)
     ("720p8", 8, 720, 1280), ("720p2", 2, 720, 1280), ("1440p2", 2, 1440, 2560),
     ("1440p1", 1, 1440, 2560), ("4k3", 3, 2160, 3840), ("1080p12", 12, 1080, 1920),
     ("kitti8", 8, 375, 1242), ("5k1", 1, 2880, 5120),
+    # config 5's extended 2-D blocks (blocks.plan2d, chunks 48/96): N = 8
+    # (2 x 4) and N = 4 (2 x 2) interior blocks of levels 0 and 1, N = 2
+    ("blk8_l0", 1, 2256, 2112), ("blk8_l1", 1, 1272, 1344), ("blk4_l0", 1, 2256, 3936),
+    ("blk4_l1", 1, 1272, 2112), ("blk2_l0", 1, 4320, 3936), ("blk2_l1", 1, 2160, 2112),
 ]
 
 
