@@ -33,6 +33,8 @@ SHAPES = [  # (name, batch, rows, cols)
     # (2 x 4) and N = 4 (2 x 2) interior blocks of levels 0 and 1, N = 2
     ("blk8_l0", 1, 2256, 2112), ("blk8_l1", 1, 1272, 1344), ("blk4_l0", 1, 2256, 3936),
     ("blk4_l1", 1, 1272, 2112), ("blk2_l0", 1, 4320, 3936), ("blk2_l1", 1, 2160, 2112),
+    # config 5's 8K level 0 on one GPU (two rounds of waves at 84 rows)
+    ("8k1", 1, 4320, 7680),
 ]
 
 
